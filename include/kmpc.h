@@ -1,0 +1,160 @@
+/*
+ * kmpc.h — C ABI of the MI355X-native Koopman-MPC window engine (libkmpc.so).
+ *
+ * This is the drop-in boundary for the per-window hot path of the reference
+ * (yli421/koopman-mpc-portfolio-rebalancing):
+ *
+ *   KoopmanMPCStrategy.rebalance            backtest.py:80-131
+ *     encode -> H x (step_latent, decode, extract[:N], destandardize)
+ *                                           backtest.py:99-121, model.py:756-797,839-850,
+ *                                           data_finance.py:717-742
+ *     solve_mpc_log_utility(w_prev, yhat)   mpc.py:27-117
+ *
+ * Conventions
+ *   - Every pointer argument of kmpc_rollout / kmpc_solve / kmpc_window is a DEVICE pointer owned
+ *     by the caller (e.g. torch tensor storage). Arrays are row-major and contiguous.
+ *   - Calls are stream-ordered on `stream` (a hipStream_t passed as void*; NULL = default stream),
+ *     allocate nothing, hold no global state and are re-entrant per device.
+ *   - Return value: KMPC_OK (0) or a negative KMPC_ERR_* code (argument / launch errors).
+ *     Per-problem solver outcome is reported in status[] (KMPC_STATUS_*), never as an error:
+ *     this mirrors mpc.py:107-117, where solver failure is not raised but reported through
+ *     problem.status and answered with the "hold current weights" fallback.
+ *   - No torch types cross this boundary.
+ */
+#ifndef KMPC_H
+#define KMPC_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ------------------------------------------------------------------------- */
+#define KMPC_OK               0
+#define KMPC_ERR_INVALID     -1   /* bad descriptor / null pointer                              */
+#define KMPC_ERR_UNSUPPORTED -2   /* shape outside what the kernels were built for             */
+#define KMPC_ERR_WORKSPACE   -3   /* ws_bytes smaller than kmpc_workspace_bytes()              */
+#define KMPC_ERR_LAUNCH      -4   /* a HIP launch failed (hipGetLastError)                     */
+
+/* ---- per-problem solver status (maps to cvxpy status strings, mpc.py:113) ----------------- */
+#define KMPC_STATUS_OPTIMAL            0  /* "optimal"                                         */
+#define KMPC_STATUS_OPTIMAL_INACCURATE 1  /* "optimal_inaccurate"                              */
+#define KMPC_STATUS_INFEASIBLE         2  /* "infeasible"                                      */
+#define KMPC_STATUS_UNBOUNDED          3  /* "unbounded"                                       */
+#define KMPC_STATUS_SOLVER_ERROR       4  /* "solver_error" (non-finite inputs, breakdown)     */
+
+/* Maximum horizon / asset count the solver kernels are instantiated for. */
+#define KMPC_MAX_H 32
+#define KMPC_MAX_N 1024
+
+/* ---- MPC solve: replaces solve_mpc_log_utility (mpc.py:27-117) ---------------------------- */
+/*
+ * For each problem b (one rolling window):
+ *   maximize_W  sum_t log(R_t . w_t) - c * sum_t ||w_t - w_{t-1}||_1        (mpc.py:66-103)
+ *   s.t.        1^T w_t = 1;  w_t >= 0 unless allow_short;                  (mpc.py:83-86)
+ *               ||w_t - w_{t-1}||_1 <= tau  if tau > 0, w_{-1} = w_prev     (mpc.py:94-100)
+ *   with R_t = exp(yhat_t) (mpc.py:55), W in [H, N].
+ * Inputs:  yhat [B, H, N] float32 (predicted log-returns, the reference passes float32 here,
+ *          backtest.py:121), w_prev [B, N] float64 (current_weights).
+ * Outputs: w_out [B, N] (W[0], what rebalance() applies, backtest.py:131) or [B, H, N] when
+ *          return_full_W != 0; status [B]; obj [B] (problem.value, NaN when not optimal);
+ *          iters [B] (may be NULL).
+ * Failure fallback (mpc.py:113-115) is applied in-kernel: w_out = tile(w_prev), obj = NaN.
+ */
+typedef struct kmpc_solve_desc {
+    int    B;              /* number of independent problems (windows)           */
+    int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */
+    int    H;              /* horizon, 1 <= H <= KMPC_MAX_H                       */
+    double cost_coeff;     /* MPCConfig.cost_coeff   (mpc.py:22)                  */
+    double max_turnover;   /* MPCConfig.max_turnover (mpc.py:23); <= 0 disables   */
+    int    allow_short;    /* MPCConfig.allow_short  (mpc.py:24)                  */
+    int    max_iter;       /* interior-point iteration cap (0 -> default 60)      */
+    double tol;            /* complementarity tolerance (<= 0 -> default 1e-10)   */
+    int    return_full_W;  /* 0: w_out is [B,N] (W[0]); 1: w_out is [B,H,N]       */
+} kmpc_solve_desc;
+
+int kmpc_solve(const kmpc_solve_desc* desc,
+               const float*  yhat,     /* [B,H,N] */
+               const double* w_prev,   /* [B,N]   */
+               double*       w_out,    /* [B,N] or [B,H,N] */
+               int*          status,   /* [B] */
+               double*       obj,      /* [B] */
+               int*          iters,    /* [B] or NULL */
+               void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- Koopman rollout: replaces backtest.py:99-121 (+ model.py encode/step/decode) ---------- */
+#define KMPC_MODEL_GENERIC 0   /* GenericKM / SparseKM (model.py:701-797)                      */
+#define KMPC_MODEL_LISTA   1   /* LISTAKM              (model.py:801-870)                      */
+#define KMPC_ACT_RELU 0
+#define KMPC_ACT_TANH 1
+#define KMPC_ACT_GELU 2
+#define KMPC_NORM_ID   0
+#define KMPC_NORM_BALL 1
+#define KMPC_MAX_LAYERS 8
+
+/*
+ * An MLP (model.py:67-117, MLPCoder): n_layers Linear layers with dims[0] -> dims[1] -> ... ->
+ * dims[n_layers]; activation `act` after every layer but the last; ReLU after the last one when
+ * last_relu. weights[l] is the nn.Linear weight [dims[l+1], dims[l]] (row-major, [out, in]),
+ * bias[l] is [dims[l+1]] or NULL.
+ */
+typedef struct kmpc_mlp {
+    int n_layers;
+    int dims[KMPC_MAX_LAYERS + 1];
+    int act;
+    int last_relu;
+    const float* weight[KMPC_MAX_LAYERS];
+    const float* bias[KMPC_MAX_LAYERS];
+} kmpc_mlp;
+
+typedef struct kmpc_rollout_desc {
+    int B;            /* windows                                                  */
+    int N;            /* assets (first N outputs of the decoder, data_finance.py:729) */
+    int H;            /* horizon                                                  */
+    int L;            /* latent size (MODEL.TARGET_SIZE)                          */
+    int obs;          /* observation size N * EMBEDDING_DIM                       */
+    int model_kind;   /* KMPC_MODEL_*                                             */
+    int norm_fn;      /* KMPC_NORM_* (GenericKM only, model.py:740-754)           */
+    /* encoder: GenericKM MLP encoder, or LISTA's We (MLP, or 1 linear layer)      */
+    kmpc_mlp encoder;
+    /* LISTA (model.py:190-209): z = shrink(We x, thr); loops x z = shrink(z S + c, thr) */
+    const float* lista_S;     /* [L, L]   */
+    int   lista_loops;
+    float lista_thresh;       /* alpha / L */
+    /* Koopman matrix, z <- z @ K (row-vector convention, model.py:311-321) */
+    const float* kmat;        /* [L, L]   */
+    /* decoder (GenericKM: MLP decoder; LISTAKM: one linear layer = normalised dictionary^T).
+       Only the first N outputs of the last layer are evaluated. For a 1-layer decoder
+       decoder.weight[0] may point at the first N rows of the [obs, L] weight (ld = L).   */
+    kmpc_mlp decoder;
+    const float* mean;        /* [N] de-standardisation (data_finance.py:740-742) */
+    const float* std;         /* [N] */
+} kmpc_rollout_desc;
+
+int kmpc_rollout(const kmpc_rollout_desc* desc,
+                 const float* obs,    /* [B, obs] standardized time-delay embedding */
+                 float*       yhat,   /* [B, H, N] */
+                 void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- fused window: rollout -> solve on one stream (KoopmanMPCStrategy.rebalance) ---------- */
+int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc,
+                const float*  obs,      /* [B, obs] */
+                const double* w_prev,   /* [B, N]   */
+                float*        yhat,     /* [B, H, N] (written; may be NULL -> kept in workspace) */
+                double*       w_out, int* status, double* obj, int* iters,
+                void* workspace, size_t ws_bytes, void* stream);
+
+/* Workspace needed by kmpc_rollout / kmpc_solve / kmpc_window (either desc may be NULL). */
+size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc);
+
+/* Human-readable text for a return code or (status + 100) for a per-problem status. */
+const char* kmpc_strerror(int code);
+
+/* Library version string. */
+const char* kmpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMPC_H */

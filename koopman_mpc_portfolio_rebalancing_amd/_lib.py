@@ -1,0 +1,102 @@
+"""ctypes binding of libkmpc.so (the C ABI declared in include/kmpc.h).
+
+The library is built in-tree (``python -m koopman_mpc_portfolio_rebalancing_amd.build`` or
+``__graft_entry__.build()``). There is no CPU fallback: if the library or a GPU is missing, the
+product path raises :class:`KmpcError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first so libkmpc.so binds to the same one)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkmpc.so")
+
+KMPC_OK = 0
+KMPC_MAX_LAYERS = 8
+KMPC_MAX_N = 1024
+KMPC_MAX_H = 21          # the Schur system (3H rows) is factored by one 64-lane wavefront
+
+MODEL_GENERIC, MODEL_LISTA = 0, 1
+ACT = {"relu": 0, "tanh": 1, "gelu": 2}
+NORM = {"id": 0, "ball": 1}
+
+STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
+                4: "solver_error"}
+
+EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
+                    "kmpc_strerror", "kmpc_version")
+
+
+class KmpcError(RuntimeError):
+    pass
+
+
+class SolveDesc(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_int),
+                ("cost_coeff", ctypes.c_double), ("max_turnover", ctypes.c_double),
+                ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
+                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int)]
+
+
+class Mlp(ctypes.Structure):
+    _fields_ = [("n_layers", ctypes.c_int), ("dims", ctypes.c_int * (KMPC_MAX_LAYERS + 1)),
+                ("act", ctypes.c_int), ("last_relu", ctypes.c_int),
+                ("weight", ctypes.c_void_p * KMPC_MAX_LAYERS),
+                ("bias", ctypes.c_void_p * KMPC_MAX_LAYERS)]
+
+
+class RolloutDesc(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_int), ("L", ctypes.c_int),
+                ("obs", ctypes.c_int), ("model_kind", ctypes.c_int), ("norm_fn", ctypes.c_int),
+                ("encoder", Mlp), ("lista_S", ctypes.c_void_p), ("lista_loops", ctypes.c_int),
+                ("lista_thresh", ctypes.c_float), ("kmat", ctypes.c_void_p), ("decoder", Mlp),
+                ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libkmpc.so (raises KmpcError if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise KmpcError(f"{p} not found: build it with `python -m koopman_mpc_portfolio_rebalancing_amd.build`")
+    L = ctypes.CDLL(p)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.kmpc_solve.argtypes = [ctypes.POINTER(SolveDesc), vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.kmpc_solve.restype = ctypes.c_int
+    L.kmpc_rollout.argtypes = [ctypes.POINTER(RolloutDesc), vp, vp, vp, sz, vp]
+    L.kmpc_rollout.restype = ctypes.c_int
+    L.kmpc_window.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc), vp, vp, vp, vp,
+                              vp, vp, vp, vp, sz, vp]
+    L.kmpc_window.restype = ctypes.c_int
+    L.kmpc_workspace_bytes.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc)]
+    L.kmpc_workspace_bytes.restype = ctypes.c_size_t
+    L.kmpc_strerror.argtypes = [ctypes.c_int]
+    L.kmpc_strerror.restype = ctypes.c_char_p
+    L.kmpc_version.argtypes = []
+    L.kmpc_version.restype = ctypes.c_char_p
+    if path is None:
+        _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != KMPC_OK:
+        msg = load().kmpc_strerror(rc).decode()
+        raise KmpcError(f"libkmpc call failed: {msg} ({rc})")
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t: torch.Tensor) -> None:
+    if not t.is_cuda:
+        raise KmpcError("libkmpc kernels need device (HIP) tensors; got a CPU tensor")

@@ -1,0 +1,92 @@
+// kmpc_capi.hip — the extern "C" boundary of libkmpc.so (declared in include/kmpc.h).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kmpc_internal.h"
+
+namespace {
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int check_solve(const kmpc_solve_desc* d) {
+    if (!d) return KMPC_ERR_INVALID;
+    if (d->B < 0 || d->N < 1 || d->H < 1) return KMPC_ERR_INVALID;
+    if (d->N > KMPC_MAX_N || d->H > KMPC_MAX_H) return KMPC_ERR_UNSUPPORTED;
+    if (d->H > 21) return KMPC_ERR_UNSUPPORTED;   // Schur system (3H) must fit one wavefront
+    return KMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kmpc_version(void) { return "kmpc 0.1.0 (gfx950)"; }
+
+const char* kmpc_strerror(int code) {
+    switch (code) {
+        case KMPC_OK: return "ok";
+        case KMPC_ERR_INVALID: return "invalid argument";
+        case KMPC_ERR_UNSUPPORTED: return "unsupported shape";
+        case KMPC_ERR_WORKSPACE: return "workspace too small";
+        case KMPC_ERR_LAUNCH: return "HIP launch failed";
+        case 100 + KMPC_STATUS_OPTIMAL: return "optimal";
+        case 100 + KMPC_STATUS_OPTIMAL_INACCURATE: return "optimal_inaccurate";
+        case 100 + KMPC_STATUS_INFEASIBLE: return "infeasible";
+        case 100 + KMPC_STATUS_UNBOUNDED: return "unbounded";
+        case 100 + KMPC_STATUS_SOLVER_ERROR: return "solver_error";
+        default: return "unknown";
+    }
+}
+
+size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc) {
+    size_t bytes = 0;
+    if (rdesc) bytes += kmpc::rollout_workspace_bytes(rdesc);
+    if (rdesc && sdesc) bytes += align256(sizeof(float) * (size_t)rdesc->B * rdesc->H * rdesc->N);
+    return bytes;
+}
+
+int kmpc_solve(const kmpc_solve_desc* desc, const float* yhat, const double* w_prev, double* w_out,
+               int* status, double* obj, int* iters, void* workspace, size_t ws_bytes,
+               void* stream) {
+    (void)workspace; (void)ws_bytes;
+    int rc = check_solve(desc);
+    if (rc) return rc;
+    if (desc->B == 0) return KMPC_OK;
+    if (!yhat || !w_prev || !w_out || !status || !obj) return KMPC_ERR_INVALID;
+    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, (hipStream_t)stream);
+}
+
+/* Debug entry (not part of include/kmpc.h): kmpc_solve plus a per-iteration trace of problem 0,
+   trace[4 * it + {0,1,2,3}] = (mu, dual residual, primal residual, step length). */
+int kmpc_solve_trace(const kmpc_solve_desc* desc, const float* yhat, const double* w_prev,
+                     double* w_out, int* status, double* obj, int* iters, double* trace,
+                     void* stream) {
+    int rc = check_solve(desc);
+    if (rc) return rc;
+    if (desc->B == 0) return KMPC_OK;
+    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, (hipStream_t)stream, trace);
+}
+
+int kmpc_rollout(const kmpc_rollout_desc* desc, const float* obs, float* yhat, void* workspace,
+                 size_t ws_bytes, void* stream) {
+    return kmpc::rollout_launch(desc, obs, yhat, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc, const float* obs,
+                const double* w_prev, float* yhat, double* w_out, int* status, double* obj,
+                int* iters, void* workspace, size_t ws_bytes, void* stream) {
+    if (!rdesc || !sdesc) return KMPC_ERR_INVALID;
+    int rc = check_solve(sdesc);
+    if (rc) return rc;
+    if (rdesc->B != sdesc->B || rdesc->N != sdesc->N || rdesc->H != sdesc->H) return KMPC_ERR_INVALID;
+    if (ws_bytes < kmpc_workspace_bytes(rdesc, sdesc)) return KMPC_ERR_WORKSPACE;
+    const size_t rbytes = kmpc::rollout_workspace_bytes(rdesc);
+    float* y = yhat ? yhat : (float*)((char*)workspace + rbytes);
+    rc = kmpc::rollout_launch(rdesc, obs, y, workspace, rbytes, (hipStream_t)stream);
+    if (rc) return rc;
+    if (sdesc->B == 0) return KMPC_OK;
+    return kmpc::solve_launch(sdesc, y, w_prev, w_out, status, obj, iters, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,19 @@
+// kmpc_internal.h — launch entry points shared by the kernels and the C ABI (kmpc_capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/kmpc.h"
+
+namespace kmpc {
+
+// kmpc_solve.hip
+int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_prev, double* w_out,
+                 int* status, double* obj, int* iters, hipStream_t stream,
+                 double* trace = nullptr);
+
+// kmpc_rollout.hip
+size_t rollout_workspace_bytes(const kmpc_rollout_desc* d);
+int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, void* ws,
+                   size_t ws_bytes, hipStream_t stream);
+
+}  // namespace kmpc

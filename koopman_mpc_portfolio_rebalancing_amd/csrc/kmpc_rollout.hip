@@ -1,0 +1,326 @@
+// kmpc_rollout.hip — batched Koopman rollout on gfx950 (replaces backtest.py:99-121).
+//
+//   z  = encode(obs)                       GenericKM: MLPCoder (model.py:108-117) + norm_fn
+//                                          LISTAKM:   LISTA (model.py:190-209)
+//   for k in 0..H-1:
+//     z = z @ K  (+ norm_fn)               model.py:311-321 / 787-797 (row-vector convention)
+//     yhat[:, k, :] = decode(z)[:, :N] * std + mean      model.py:768-777 / 839-850,
+//                                          data_finance.py:729 (slice), :740-742 (de-standardize)
+//
+// Every dense contraction is one fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32: exact fp32 products,
+// fp32 accumulation, the arithmetic type of the reference's torch fp32 path) with a fused epilogue
+// (bias + activation, LISTA shrink, de-standardize-and-scatter). Only the first N decoder rows are
+// evaluated. Weights in the reference's nn.Linear [out, in] layout are consumed as-is ("NT");
+// K and S (right-multiplied, [in, out]) are transposed once per call into the workspace.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kmpc_internal.h"
+
+namespace kmpc {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum Epi : int {
+    EPI_NONE = 0,        // out = acc (+ bias)
+    EPI_ACT = 1,         // out = act(acc + bias)
+    EPI_SHRINK = 2,      // out = shrink(acc + R, thr)            (LISTA, model.py:30-40,205-207)
+    EPI_DESTD = 3,       // out = acc * std[n] + mean[n]          (data_finance.py:740-742)
+};
+
+struct GemmArgs {
+    int M, N, K;
+    const float* A; int lda;      // [M, K]
+    const float* B; int ldb;      // [N, K]  (nn.Linear weight layout)
+    const float* bias;            // [N] or null
+    float* C; int ldc;            // [M, N] (row stride ldc)
+    int epi, act;
+    const float* R; int ldr;      // EPI_SHRINK addend [M, N]
+    float thr;
+    const float* mean; const float* stdv;   // EPI_DESTD [N]
+};
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float apply_act(float x, int act) {
+    if (act == KMPC_ACT_RELU) return fmaxf(x, 0.0f);
+    if (act == KMPC_ACT_TANH) return tanhf(x);
+    return gelu_erf(x);
+}
+
+// Tile: 128 x 128 outputs per 256-thread block (4 waves, 2 x 2 of 64 x 64), BK = 32.
+constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
+
+// C = epi(A . B^T). Each lane of an MFMA consumes 16 contiguous k (k = 16h + s, h = lane >> 5),
+// so operand fragments are two ds_read_b128 per row; the k permutation is the same for A and B.
+__global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
+    __shared__ float As[BM * LDS_STRIDE];
+    __shared__ float Bs[BN * LDS_STRIDE];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+    const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
+                        ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+        // stage A and B tiles: 128 rows x 32 k = 1024 float4 per operand, 4 per thread
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int idx = tid + q * 256;          // 0..1023
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int kk = k0 + c4;
+            f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+            const int ma = m0 + row, nb = n0 + row;
+            if (vec_ok && kk + 3 < g.K) {
+                if (ma < g.M) va = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
+                if (nb < g.N) vb = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (kk + e < g.K) {
+                        if (ma < g.M) va[e] = g.A[(size_t)ma * g.lda + kk + e];
+                        if (nb < g.N) vb[e] = g.B[(size_t)nb * g.ldb + kk + e];
+                    }
+                }
+            }
+            *(f32x4*)(As + row * LDS_STRIDE + c4) = va;
+            *(f32x4*)(Bs + row * LDS_STRIDE + c4) = vb;
+        }
+        __syncthreads();
+        const int r = lane & 31, h = lane >> 5;
+        float af[2][16], bf[2][16];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const float* pa = As + (wm + a * 32 + r) * LDS_STRIDE + 16 * h;
+            const float* pb = Bs + (wn + a * 32 + r) * LDS_STRIDE + 16 * h;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 x = *(const f32x4*)(pa + 4 * q);
+                const f32x4 y = *(const f32x4*)(pb + 4 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { af[a][4 * q + e] = x[e]; bf[a][4 * q + e] = y[e]; }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+        __syncthreads();
+    }
+    // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int n = n0 + wn + b * 32 + (lane & 31);
+            if (n >= g.N) continue;
+            const float bias = g.bias ? g.bias[n] : 0.0f;
+            float mu = 0.0f, sd = 1.0f;
+            if (g.epi == EPI_DESTD) { mu = g.mean[n]; sd = g.stdv[n]; }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m >= g.M) continue;
+                float v = acc[a][b][r] + bias;
+                if (g.epi == EPI_ACT) {
+                    v = apply_act(v, g.act);
+                } else if (g.epi == EPI_SHRINK) {
+                    v += g.R[(size_t)m * g.ldr + n];
+                    const float av = fabsf(v) - g.thr;
+                    v = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
+                } else if (g.epi == EPI_DESTD) {
+                    v = v * sd + mu;
+                }
+                g.C[(size_t)m * g.ldc + n] = v;
+            }
+        }
+}
+
+// shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
+__global__ void shrink_kernel(const float* x, float* y, size_t n, float thr) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float v = x[i];
+        const float av = fabsf(v) - thr;
+        y[i] = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
+    }
+}
+
+// x / ||x||_2 per row (norm_fn 'ball', model.py:750-751); one wave per row
+__global__ void ball_norm_kernel(float* x, int M, int L) {
+    const int row = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64, lane = threadIdx.x & 63;
+    if (row >= M) return;
+    float* p = x + (size_t)row * L;
+    float s = 0.0f;
+    for (int j = lane; j < L; j += 64) s += p[j] * p[j];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float nrm = sqrtf(s);
+    for (int j = lane; j < L; j += 64) p[j] = p[j] / nrm;
+}
+
+// out[j][i] = in[i][j]  (L x L)
+__global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
+    __shared__ float tile[32][33];
+    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 8 rows per pass
+    for (int r = ty; r < 32; r += 8) {
+        const int i = by + r, j = bx + tx;
+        if (i < R && j < Cc) tile[r][tx] = in[(size_t)i * Cc + j];
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int j = bx + r, i = by + tx;
+        if (i < R && j < Cc) out[(size_t)j * R + i] = tile[tx][r];
+    }
+}
+
+static int gemm(const GemmArgs& g, hipStream_t s) {
+    if (g.M <= 0 || g.N <= 0) return KMPC_OK;
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
+    hipLaunchKernelGGL(gemm_nt_kernel, grid, dim3(256), 0, s, g);
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+static GemmArgs linear(int M, int N, int K, const float* A, int lda, const float* W, const float* bias,
+                       float* C, int ldc) {
+    GemmArgs g = {};
+    g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias;
+    g.C = C; g.ldc = ldc; g.epi = EPI_NONE;
+    return g;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int max_width(const kmpc_mlp& m) {
+    int w = 0;
+    for (int l = 0; l <= m.n_layers; ++l) w = m.dims[l] > w ? m.dims[l] : w;
+    return w;
+}
+
+size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
+    if (!d) return 0;
+    const size_t B = (size_t)d->B;
+    int wmax = d->L;
+    const int we = max_width(d->encoder), wd = max_width(d->decoder);
+    if (we > wmax) wmax = we;
+    if (wd > wmax) wmax = wd;
+    size_t bytes = 0;
+    bytes += align256(sizeof(float) * (size_t)d->L * d->L);        // K^T
+    bytes += align256(sizeof(float) * (size_t)d->L * d->L);        // S^T (LISTA)
+    bytes += 2 * align256(sizeof(float) * B * wmax);               // ping-pong activations
+    bytes += 2 * align256(sizeof(float) * B * d->L);               // z, c (LISTA) / z next
+    return bytes;
+}
+
+// run an MLP on X [B, dims[0]] -> out [B, dims[n]] (only the first `last_cols` outputs of the last
+// layer, written with row stride ldo); ping/pong are [B, wmax] scratch buffers.
+static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* out, int ldo,
+                   int last_cols, int last_epi, const float* mean, const float* stdv, float* ping,
+                   float* pong, int wmax, hipStream_t s) {
+    const float* cur = X;
+    int ldc = ldx;
+    for (int l = 0; l < m.n_layers; ++l) {
+        const bool last = (l == m.n_layers - 1);
+        const int nout = last ? last_cols : m.dims[l + 1];
+        float* dst = last ? out : ((l & 1) ? pong : ping);
+        GemmArgs g = linear(Bn, nout, m.dims[l], cur, ldc, m.weight[l], m.bias[l], dst,
+                            last ? ldo : wmax);
+        if (!last) { g.epi = EPI_ACT; g.act = m.act; }
+        else if (last_epi == EPI_DESTD) { g.epi = EPI_DESTD; g.mean = mean; g.stdv = stdv; }
+        else if (m.last_relu) { g.epi = EPI_ACT; g.act = KMPC_ACT_RELU; }
+        int rc = gemm(g, s);
+        if (rc) return rc;
+        cur = dst;
+        ldc = wmax;
+    }
+    return KMPC_OK;
+}
+
+int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, void* ws,
+                   size_t ws_bytes, hipStream_t s) {
+    if (!d || !obs || !yhat || !d->kmat || !d->mean || !d->std) return KMPC_ERR_INVALID;
+    if (d->B < 0 || d->N < 1 || d->H < 1 || d->L < 1 || d->obs < d->N) return KMPC_ERR_INVALID;
+    if (d->encoder.n_layers < 1 || d->encoder.n_layers > KMPC_MAX_LAYERS) return KMPC_ERR_INVALID;
+    if (d->decoder.n_layers < 1 || d->decoder.n_layers > KMPC_MAX_LAYERS) return KMPC_ERR_INVALID;
+    if (d->encoder.dims[0] != d->obs || d->encoder.dims[d->encoder.n_layers] != d->L) return KMPC_ERR_INVALID;
+    if (d->decoder.dims[0] != d->L || d->decoder.dims[d->decoder.n_layers] < d->N) return KMPC_ERR_INVALID;
+    if (d->model_kind == KMPC_MODEL_LISTA && !d->lista_S) return KMPC_ERR_INVALID;
+    if (ws_bytes < rollout_workspace_bytes(d) || (!ws && ws_bytes)) return KMPC_ERR_WORKSPACE;
+    if (d->B == 0) return KMPC_OK;
+    const int Bn = d->B, L = d->L, N = d->N, H = d->H;
+    int wmax = L;
+    {
+        const int we = max_width(d->encoder), wd = max_width(d->decoder);
+        if (we > wmax) wmax = we;
+        if (wd > wmax) wmax = wd;
+    }
+    char* p = (char*)ws;
+    float* Kt = (float*)p;   p += align256(sizeof(float) * (size_t)L * L);
+    float* St = (float*)p;   p += align256(sizeof(float) * (size_t)L * L);
+    float* ping = (float*)p; p += align256(sizeof(float) * (size_t)Bn * wmax);
+    float* pong = (float*)p; p += align256(sizeof(float) * (size_t)Bn * wmax);
+    float* z0 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
+    float* z1 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
+    int rc;
+    dim3 tg((L + 31) / 32, (L + 31) / 32);
+    hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
+    if (d->model_kind == KMPC_MODEL_LISTA)
+        hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->lista_S, St, L, L);
+    if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
+
+    // ---- encode ----
+    if (d->model_kind == KMPC_MODEL_GENERIC) {
+        rc = run_mlp(d->encoder, Bn, obs, d->obs, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        if (rc) return rc;
+        if (d->norm_fn == KMPC_NORM_BALL)
+            hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, z0, Bn, L);
+    } else {
+        // c = We(x) (z1 holds c), z = shrink(c); loops: z = shrink(z S + c)   (model.py:200-209)
+        rc = run_mlp(d->encoder, Bn, obs, d->obs, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        if (rc) return rc;
+        const size_t n = (size_t)Bn * L;
+        hipLaunchKernelGGL(shrink_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z1, z0, n,
+                           d->lista_thresh);
+        float* zc = z0;
+        float* zn = ping;   // ping is [B, wmax] >= [B, L]
+        for (int it = 0; it < d->lista_loops; ++it) {
+            GemmArgs g = linear(Bn, L, L, zc, L, St, nullptr, zn, L);
+            g.epi = EPI_SHRINK; g.R = z1; g.ldr = L; g.thr = d->lista_thresh;
+            if ((rc = gemm(g, s))) return rc;
+            float* t = zc; zc = zn; zn = t;
+        }
+        if (zc != z0) hipMemcpyAsync(z0, zc, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+    }
+    if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
+
+    // ---- H x (step_latent, decode[:N], destandardize) ----
+    float* zc = z0;
+    float* zn = z1;
+    for (int k = 0; k < H; ++k) {
+        GemmArgs g = linear(Bn, L, L, zc, L, Kt, nullptr, zn, L);
+        if ((rc = gemm(g, s))) return rc;
+        if (d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL)
+            hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, zn, Bn, L);
+        // decoder: hidden layers full width, last layer first-N rows + destandardize into yhat[:, k, :]
+        rc = run_mlp(d->decoder, Bn, zn, L, yhat + (size_t)k * N, H * N, N, EPI_DESTD, d->mean, d->std,
+                     ping, pong, wmax, s);
+        if (rc) return rc;
+        float* t = zc; zc = zn; zn = t;
+    }
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+}  // namespace kmpc

@@ -1,0 +1,118 @@
+"""MPC solve — the reference's ``mpc.py`` API on the gfx950 solver kernel.
+
+Mirrors ``MPCConfig`` (mpc.py:17-25) field for field and ``solve_mpc_log_utility``
+(mpc.py:27-117) signature, return shapes/dtypes and failure semantics: solver failure is never
+raised; a status outside {"optimal", "optimal_inaccurate"} returns ``tile(current_weights)`` and
+``{"status": s, "value": None}`` (mpc.py:113-115).
+
+``solve_mpc_log_utility_batched`` is the batched entry point (torch device tensors in and out)
+that the strategies and the benchmark use.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+@dataclass
+class MPCConfig:
+    """Configuration for MPC solver (mpc.py:17-25)."""
+    horizon: int = 5
+    gamma: float = 0.0  # Risk aversion (0.0 = log utility maximization); unused by log utility
+    cost_coeff: float = 0.001  # Transaction cost coefficient (e.g. 10bps)
+    max_turnover: float = 0.2  # Maximum turnover per step
+    allow_short: bool = False
+    solver: str = "ECOS"  # accepted for compatibility; the gfx950 interior-point kernel solves
+    # extra (defaulted) knobs of the device solver
+    max_iter: int = 80
+    tol: float = 1e-11
+
+
+def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:
+    d = _lib.SolveDesc()
+    d.B, d.N, d.H = int(B), int(N), int(H)
+    d.cost_coeff = float(config.cost_coeff)
+    d.max_turnover = float(config.max_turnover)
+    d.allow_short = int(bool(config.allow_short))
+    d.max_iter = int(getattr(config, "max_iter", 80))
+    d.tol = float(getattr(config, "tol", 1e-11))
+    d.return_full_W = int(bool(full))
+    return d
+
+
+def solve_mpc_log_utility_batched(
+    current_weights: torch.Tensor,
+    predicted_log_returns: torch.Tensor,
+    config: MPCConfig,
+    return_full: bool = False,
+    with_iters: bool = False,
+):
+    """Batched solve on the device.
+
+    Args:
+        current_weights: [B, N] (float64; other dtypes are converted) device tensor.
+        predicted_log_returns: [B, H, N] float32 device tensor (the reference feeds float32 yhat).
+        config: MPCConfig.
+        return_full: return W [B, H, N] instead of W[:, 0] [B, N].
+
+    Returns:
+        (W, status, value[, iters]): W float64, status int32 [B] (see _lib.STATUS_NAMES),
+        value float64 [B] (NaN where the fallback was applied).
+    """
+    y = predicted_log_returns
+    _lib.require_gpu(y)
+    if y.dim() != 3:
+        raise ValueError("predicted_log_returns must be [B, H, N]")
+    B, H, N = y.shape
+    y = y.to(torch.float32).contiguous()
+    wp = current_weights.to(device=y.device, dtype=torch.float64).contiguous()
+    if wp.shape != (B, N):
+        raise ValueError(f"current_weights must be [{B}, {N}], got {tuple(wp.shape)}")
+    if H > _lib.KMPC_MAX_H or N > _lib.KMPC_MAX_N:
+        raise _lib.KmpcError(f"shape H={H}, N={N} exceeds the kernel limits "
+                             f"(H <= {_lib.KMPC_MAX_H}, N <= {_lib.KMPC_MAX_N})")
+    W = torch.empty((B, H, N) if return_full else (B, N), dtype=torch.float64, device=y.device)
+    status = torch.empty(B, dtype=torch.int32, device=y.device)
+    value = torch.empty(B, dtype=torch.float64, device=y.device)
+    iters = torch.empty(B, dtype=torch.int32, device=y.device)
+    d = _solve_desc(B, N, H, config, return_full)
+    L = _lib.load()
+    with torch.cuda.device(y.device):
+        rc = L.kmpc_solve(ctypes.byref(d), y.data_ptr(), wp.data_ptr(), W.data_ptr(),
+                          status.data_ptr(), value.data_ptr(), iters.data_ptr(), None, 0,
+                          _lib.stream_handle(y.device))
+    _lib.check(rc)
+    if with_iters:
+        return W, status, value, iters
+    return W, status, value
+
+
+def _default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise _lib.KmpcError("solve_mpc_log_utility runs on the gfx950 kernel and needs a GPU")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def solve_mpc_log_utility(
+    current_weights: np.ndarray,
+    predicted_log_returns: np.ndarray,
+    config: MPCConfig,
+) -> Tuple[np.ndarray, Dict]:
+    """Drop-in for mpc.py:27-117: returns (W [H, N] float64, {"status", "value"})."""
+    y = np.asarray(predicted_log_returns)
+    H, N = y.shape
+    dev = _default_device()
+    yt = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float32), device=dev).reshape(1, H, N)
+    wt = torch.as_tensor(np.asarray(current_weights, dtype=np.float64), device=dev).reshape(1, N)
+    W, status, value = solve_mpc_log_utility_batched(wt, yt, config, return_full=True)
+    st = _lib.STATUS_NAMES.get(int(status.item()), "solver_error")
+    W_np = W[0].cpu().numpy()
+    if st not in ("optimal", "optimal_inaccurate"):
+        return np.tile(np.asarray(current_weights, dtype=np.float64), (H, 1)), {"status": st, "value": None}
+    return W_np, {"status": st, "value": float(value.item())}
