@@ -45,7 +45,7 @@ extern "C" {
 #define KMPC_STATUS_SOLVER_ERROR       4  /* "solver_error" (non-finite inputs, breakdown)     */
 
 /* Maximum horizon / asset count the solver kernels are instantiated for. */
-#define KMPC_MAX_H 32
+#define KMPC_MAX_H 21   /* the 3H x 3H Schur system is factored by one 64-lane wavefront */
 #define KMPC_MAX_N 1024
 
 /* ---- MPC solve: replaces solve_mpc_log_utility (mpc.py:27-117) ---------------------------- */
@@ -69,9 +69,10 @@ typedef struct kmpc_solve_desc {
     double cost_coeff;     /* MPCConfig.cost_coeff   (mpc.py:22)                  */
     double max_turnover;   /* MPCConfig.max_turnover (mpc.py:23); <= 0 disables   */
     int    allow_short;    /* MPCConfig.allow_short  (mpc.py:24)                  */
-    int    max_iter;       /* interior-point iteration cap (0 -> default 60)      */
-    double tol;            /* complementarity tolerance (<= 0 -> default 1e-10)   */
+    int    max_iter;       /* interior-point iteration cap (0 -> default 80)      */
+    double tol;            /* complementarity tolerance (<= 0 -> default 1e-11)   */
     int    return_full_W;  /* 0: w_out is [B,N] (W[0]); 1: w_out is [B,H,N]       */
+    int    n_refine;       /* iterative-refinement steps per Newton solve (<0 -> 0, 0 -> default 2) */
 } kmpc_solve_desc;
 
 int kmpc_solve(const kmpc_solve_desc* desc,

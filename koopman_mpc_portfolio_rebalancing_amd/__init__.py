@@ -1,4 +1,13 @@
-"""MI355X-native Koopman-MPC window engine (drop-in for the reference's mpc/backtest hot path)."""
+"""MI355X-native Koopman-MPC window engine.
+
+Drop-in for the reference's per-window hot path (yli421/koopman-mpc-portfolio-rebalancing):
+``MPCConfig`` / ``solve_mpc_log_utility`` (mpc.py) and ``BacktestConfig`` / ``Strategy`` /
+``BuyAndHoldStrategy`` / ``KoopmanMPCStrategy`` / ``run_backtest`` / ``calculate_metrics``
+(backtest.py), executed by hand-written gfx950 kernels in libkmpc.so (C ABI: include/kmpc.h).
+"""
 from .mpc import MPCConfig, solve_mpc_log_utility, solve_mpc_log_utility_batched  # noqa: F401
+from .koopman import DeviceKoopman, KoopmanModelSpec  # noqa: F401
+from .backtest import (BacktestConfig, BuyAndHoldStrategy, KoopmanMPCStrategy, Strategy,  # noqa: F401
+                       calculate_metrics, run_backtest)
 
 __version__ = "0.1.0"

@@ -38,7 +38,7 @@ class SolveDesc(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_int),
                 ("cost_coeff", ctypes.c_double), ("max_turnover", ctypes.c_double),
                 ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
-                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int)]
+                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int), ("n_refine", ctypes.c_int)]
 
 
 class Mlp(ctypes.Structure):

@@ -888,7 +888,7 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
             __syncthreads();
             const int ncon = (T.hw ? H * N : 0) + (T.hs ? 2 * H * N : 0) + (T.ht ? H : 0);
             const double inv_ncon = 1.0 / (ncon > 0 ? ncon : 1);
-            double best = 1e300, best_pr = 1e300, best_dr = 1e300, best_mu = 1e300;
+            double best = 1e300, best_pr = 1e300, best_dr = 1e300, best_mu = 1e300, min_pr = 1e300;
 
             for (it = 0; it < args.max_iter; ++it) {
                 // ---- residuals: den_t = 1 + m.w, 1'w_t - 1, tau - 1's_t - z4 ----
@@ -939,6 +939,7 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 }
                 mu *= inv_ncon;
                 const double merit = fmax(mu, fmax(rd, pr));
+                min_pr = fmin(min_pr, pr);
                 if (args.trace && b == 0 && threadIdx.x == 0) {
                     args.trace[4 * it + 0] = mu; args.trace[4 * it + 1] = rd; args.trace[4 * it + 2] = pr;
                 }
@@ -1020,8 +1021,9 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
             }
             if (best <= 1e-7) status = KMPC_STATUS_OPTIMAL;
             else if (best <= 1e-4) status = KMPC_STATUS_OPTIMAL_INACCURATE;
-            else if (best_pr > fmax(best_mu, best_dr)) status = KMPC_STATUS_INFEASIBLE;
+            else if (min_pr > 1e-6) status = KMPC_STATUS_INFEASIBLE;   // primal residual never closed
             else status = KMPC_STATUS_SOLVER_ERROR;
+            (void)best_pr; (void)best_dr; (void)best_mu;
         }
     }
     __syncthreads();
@@ -1059,7 +1061,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.max_iter = d->max_iter > 0 ? d->max_iter : 80;
     a.tol = d->tol > 0.0 ? d->tol : 1e-11;
     a.return_full = d->return_full_W;
-    a.n_refine = 1;
+    a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 2);
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;

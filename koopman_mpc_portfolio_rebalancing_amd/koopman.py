@@ -1,0 +1,224 @@
+"""Koopman model inference subset on the device (the rollout half of the window hot path).
+
+Mirrors what ``KoopmanMPCStrategy.rebalance`` uses of the reference model (backtest.py:99-121):
+``encode`` (GenericKM model.py:756-766 / LISTAKM model.py:828-837), ``step_latent``
+(model.py:311-321, 787-797), ``decode`` (model.py:768-777, 839-850), then the env's
+``extract_current_returns`` (first N outputs, data_finance.py:729) and ``destandardize_returns``
+(data_finance.py:740-742). Weights are read from the reference's ``state_dict`` layout (the
+checkpoint written by train.py:475-491), or from a live reference model object.
+
+All per-window arithmetic runs in libkmpc.so (fp32 MFMA GEMMs + fused epilogues); this module only
+arranges weight pointers (and, once per model, normalises the LISTA dictionary).
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from dataclasses import dataclass, field
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _cfg_get(cfg: Any, *path, default=None):
+    """Read cfg.MODEL.ENCODER.LAYERS style paths from a Config object or its to_dict()."""
+    cur = cfg
+    for key in path:
+        if cur is None:
+            return default
+        if isinstance(cur, dict):
+            cur = cur.get(key, None)
+        else:
+            cur = getattr(cur, key, None)
+    return default if cur is None else cur
+
+
+def _linear_stack(sd: dict, prefix: str) -> List[Tuple[torch.Tensor, Optional[torch.Tensor]]]:
+    """Collect nn.Sequential Linear layers '<prefix>.<idx>.weight/bias' in index order."""
+    pat = re.compile(re.escape(prefix) + r"\.(\d+)\.weight$")
+    idx = sorted(int(m.group(1)) for k in sd for m in [pat.match(k)] if m)
+    return [(sd[f"{prefix}.{i}.weight"], sd.get(f"{prefix}.{i}.bias")) for i in idx]
+
+
+@dataclass
+class KoopmanModelSpec:
+    """Inference description of a reference KoopmanMachine (weights as float32 tensors)."""
+    kind: str                                   # 'generic' (GenericKM / SparseKM) | 'lista' (LISTAKM)
+    encoder: List[Tuple[torch.Tensor, Optional[torch.Tensor]]]
+    kmat: torch.Tensor
+    decoder: List[Tuple[torch.Tensor, Optional[torch.Tensor]]]
+    enc_act: str = "relu"
+    enc_last_relu: bool = False
+    dec_act: str = "relu"
+    norm_fn: str = "id"
+    lista_S: Optional[torch.Tensor] = None
+    lista_loops: int = 0
+    lista_thresh: float = 0.0
+
+    @property
+    def latent(self) -> int:
+        return int(self.kmat.shape[0])
+
+    @property
+    def obs_size(self) -> int:
+        return int(self.encoder[0][0].shape[1])
+
+    @classmethod
+    def from_state_dict(cls, sd: dict, cfg: Any) -> "KoopmanModelSpec":
+        """sd: model_state_dict (train.py:478); cfg: Config or checkpoint['config'] dict."""
+        sd = {k: (v if torch.is_tensor(v) else torch.as_tensor(np.asarray(v))) for k, v in sd.items()}
+        name = _cfg_get(cfg, "MODEL", "MODEL_NAME", default="GenericKM")
+        enc_act = _cfg_get(cfg, "MODEL", "ENCODER", "ACTIVATION", default="relu")
+        enc_last_relu = bool(_cfg_get(cfg, "MODEL", "ENCODER", "LAST_RELU", default=False))
+        if name == "LISTAKM":
+            alpha = float(_cfg_get(cfg, "MODEL", "ENCODER", "LISTA", "ALPHA"))
+            L = float(_cfg_get(cfg, "MODEL", "ENCODER", "LISTA", "L"))
+            loops = int(_cfg_get(cfg, "MODEL", "ENCODER", "LISTA", "NUM_LOOPS"))
+            if "lista.We.weight" in sd:          # LINEAR_ENCODER=True: nn.Linear(bias=False)
+                enc = [(sd["lista.We.weight"], None)]
+                enc_last = False
+            else:
+                enc = _linear_stack(sd, "lista.We.network")
+                enc_last = enc_last_relu
+            d = sd["dict"].float()                                      # [L, obs]
+            wd = d / torch.linalg.norm(d, dim=1, keepdim=True).clamp(min=1e-4)   # model.py:846-850
+            return cls(kind="lista", encoder=enc, kmat=sd["kmat"], decoder=[(wd.t().contiguous(), None)],
+                       enc_act=enc_act, enc_last_relu=enc_last, lista_S=sd["lista.S"],
+                       lista_loops=loops, lista_thresh=alpha / L)
+        if name not in ("GenericKM", "SparseKM"):
+            raise ValueError(f"unknown MODEL_NAME {name!r}")
+        return cls(kind="generic", encoder=_linear_stack(sd, "encoder.network"), kmat=sd["kmat"],
+                   decoder=_linear_stack(sd, "decoder.network"), enc_act=enc_act,
+                   enc_last_relu=enc_last_relu,
+                   dec_act=_cfg_get(cfg, "MODEL", "DECODER", "ACTIVATION", default="relu"),
+                   norm_fn=_cfg_get(cfg, "MODEL", "NORM_FN", default="id"))
+
+    @classmethod
+    def from_model(cls, model: Any) -> "KoopmanModelSpec":
+        """From a live reference KoopmanMachine (uses model.cfg + model.state_dict())."""
+        return cls.from_state_dict(model.state_dict(), model.cfg)
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint: dict) -> "KoopmanModelSpec":
+        """From a train.py checkpoint dict: {'model_state_dict', 'config', ...} (train.py:475-491)."""
+        return cls.from_state_dict(checkpoint["model_state_dict"], checkpoint["config"])
+
+
+class DeviceKoopman:
+    """A KoopmanModelSpec resident on one device, evaluated through kmpc_rollout / kmpc_window."""
+
+    def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None):
+        if device is None:
+            if not torch.cuda.is_available():
+                raise _lib.KmpcError("DeviceKoopman needs a GPU (libkmpc.so has no CPU path)")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise _lib.KmpcError("DeviceKoopman needs a HIP device")
+        self.spec = spec
+
+        def up(t):
+            return None if t is None else t.detach().to(self.device, torch.float32).contiguous()
+
+        self.enc = [(up(W), up(b)) for W, b in spec.encoder]
+        self.dec = [(up(W), up(b)) for W, b in spec.decoder]
+        self.kmat = up(spec.kmat)
+        self.S = up(spec.lista_S)
+        if len(self.enc) > _lib.KMPC_MAX_LAYERS or len(self.dec) > _lib.KMPC_MAX_LAYERS:
+            raise _lib.KmpcError("too many layers for kmpc_mlp")
+        self._ws = None
+
+    @property
+    def latent(self) -> int:
+        return self.spec.latent
+
+    @property
+    def obs_size(self) -> int:
+        return self.spec.obs_size
+
+    def _mlp(self, layers, act, last_relu) -> _lib.Mlp:
+        m = _lib.Mlp()
+        m.n_layers = len(layers)
+        m.dims[0] = int(layers[0][0].shape[1])
+        for k, (W, b) in enumerate(layers):
+            m.dims[k + 1] = int(W.shape[0])
+            m.weight[k] = W.data_ptr()
+            m.bias[k] = b.data_ptr() if b is not None else None
+        m.act = _lib.ACT[act]
+        m.last_relu = int(bool(last_relu))
+        return m
+
+    def rollout_desc(self, B: int, H: int, N: int, mean: torch.Tensor, std: torch.Tensor) -> _lib.RolloutDesc:
+        d = _lib.RolloutDesc()
+        d.B, d.N, d.H, d.L, d.obs = int(B), int(N), int(H), self.latent, self.obs_size
+        s = self.spec
+        d.model_kind = _lib.MODEL_LISTA if s.kind == "lista" else _lib.MODEL_GENERIC
+        d.norm_fn = _lib.NORM[s.norm_fn]
+        d.encoder = self._mlp(self.enc, s.enc_act, s.enc_last_relu)
+        d.lista_S = self.S.data_ptr() if self.S is not None else None
+        d.lista_loops = int(s.lista_loops)
+        d.lista_thresh = float(s.lista_thresh)
+        d.kmat = self.kmat.data_ptr()
+        d.decoder = self._mlp(self.dec, s.dec_act, False)
+        d.mean = mean.data_ptr()
+        d.std = std.data_ptr()
+        return d
+
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _stats(self, mean, std, N):
+        m = torch.as_tensor(mean, dtype=torch.float32, device=self.device).reshape(-1)[:N].contiguous()
+        s = torch.as_tensor(std, dtype=torch.float32, device=self.device).reshape(-1)[:N].contiguous()
+        return m, s
+
+    def rollout(self, obs: torch.Tensor, mean, std, horizon: int, n_assets: int) -> torch.Tensor:
+        """yhat [B, H, N] float32 (predicted de-standardized log-returns) for obs [B, obs_size]."""
+        _lib.require_gpu(obs)
+        x = obs.to(self.device, torch.float32).contiguous()
+        B = x.shape[0]
+        if x.shape[1] != self.obs_size:
+            raise ValueError(f"obs width {x.shape[1]} != model observation size {self.obs_size}")
+        m, s = self._stats(mean, std, n_assets)
+        y = torch.empty((B, horizon, n_assets), dtype=torch.float32, device=self.device)
+        d = self.rollout_desc(B, horizon, n_assets, m, s)
+        L = _lib.load()
+        nbytes = L.kmpc_workspace_bytes(ctypes.byref(d), None)
+        ws = self._workspace(nbytes)
+        with torch.cuda.device(self.device):
+            rc = L.kmpc_rollout(ctypes.byref(d), x.data_ptr(), y.data_ptr(), ws.data_ptr(), nbytes,
+                                _lib.stream_handle(self.device))
+        _lib.check(rc)
+        return y
+
+    def window(self, obs: torch.Tensor, w_prev: torch.Tensor, mean, std, n_assets: int, mpc_config,
+               keep_yhat: bool = False, return_full: bool = False):
+        """Fused window (kmpc_window): obs [B, obs], w_prev [B, N] -> (W0 or W, status, value[, yhat])."""
+        from .mpc import _solve_desc
+        _lib.require_gpu(obs)
+        x = obs.to(self.device, torch.float32).contiguous()
+        B = x.shape[0]
+        H = int(mpc_config.horizon)
+        wp = w_prev.to(self.device, torch.float64).contiguous()
+        m, s = self._stats(mean, std, n_assets)
+        rd = self.rollout_desc(B, H, n_assets, m, s)
+        sd = _solve_desc(B, n_assets, H, mpc_config, return_full)
+        L = _lib.load()
+        nbytes = L.kmpc_workspace_bytes(ctypes.byref(rd), ctypes.byref(sd))
+        ws = self._workspace(nbytes)
+        y = torch.empty((B, H, n_assets), dtype=torch.float32, device=self.device) if keep_yhat else None
+        W = torch.empty((B, H, n_assets) if return_full else (B, n_assets), dtype=torch.float64, device=self.device)
+        status = torch.empty(B, dtype=torch.int32, device=self.device)
+        value = torch.empty(B, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = L.kmpc_window(ctypes.byref(rd), ctypes.byref(sd), x.data_ptr(), wp.data_ptr(),
+                               y.data_ptr() if y is not None else None, W.data_ptr(), status.data_ptr(),
+                               value.data_ptr(), None, ws.data_ptr(), nbytes,
+                               _lib.stream_handle(self.device))
+        _lib.check(rc)
+        return (W, status, value, y) if keep_yhat else (W, status, value)

@@ -32,6 +32,7 @@ class MPCConfig:
     # extra (defaulted) knobs of the device solver
     max_iter: int = 80
     tol: float = 1e-11
+    n_refine: int = 0  # 0 -> kernel default
 
 
 def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:
@@ -43,6 +44,7 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     d.max_iter = int(getattr(config, "max_iter", 80))
     d.tol = float(getattr(config, "tol", 1e-11))
     d.return_full_W = int(bool(full))
+    d.n_refine = int(getattr(config, "n_refine", 0))
     return d
 
 

@@ -512,7 +512,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
         }
         int ncon = (W.hw ? (int)HN : 0) + (W.hs ? 2 * (int)HN : 0) + (W.ht ? H : 0);
         if (ncon == 0) ncon = 1;
-        real best = R_(1e30), best_pr = R_(1e30), best_dr = R_(1e30), best_mu = R_(1e30);
+        real best = R_(1e30), best_pr = R_(1e30), best_dr = R_(1e30), best_mu = R_(1e30), min_pr = R_(1e30);
         int trace = getenv("KMPC_ORACLE_TRACE") != NULL;
 
         for (it = 0; it < max_iter; ++it) {
@@ -548,6 +548,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
             if (!domain_ok) break;
             mu /= ncon;
             real merit = RFMAX(mu, RFMAX(rd, pr));
+            min_pr = RFMIN(min_pr, pr);
             if (trace) fprintf(stderr, "it %d mu %.3Le rd %.3Le pr %.3Le\n", it, (long double)mu,
                                (long double)rd, (long double)pr);
             if (!RISFIN(merit)) break;
@@ -590,8 +591,9 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
         }
         if (best <= R_(1e-7)) status = ST_OPTIMAL;
         else if (best <= R_(1e-4)) status = ST_INACCURATE;
-        else if (best_pr > RFMAX(best_mu, best_dr)) status = ST_INFEASIBLE;
+        else if (min_pr > R_(1e-6)) status = ST_INFEASIBLE;   /* primal residual never closed */
         else status = ST_ERROR;
+        (void)best_pr; (void)best_dr; (void)best_mu;
     }
 done:
     if (iters_out) *iters_out = it;

@@ -1,0 +1,98 @@
+"""The C ABI boundary without a GPU: libkmpc.so loads, exports every function include/kmpc.h
+declares, and the ctypes mirrors match the C struct layouts (checked by compiling the header)."""
+import ctypes
+import inspect
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from koopman_mpc_portfolio_rebalancing_amd import _lib
+import koopman_mpc_portfolio_rebalancing_amd as pkg
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kmpc.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kmpc_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_function():
+    lib = _lib.load()
+    names = header_functions()
+    assert set(names) == set(_lib.EXPORTED_SYMBOLS)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.kmpc_version().decode().startswith("kmpc")
+    assert lib.kmpc_strerror(_lib.KMPC_OK).decode() == "ok"
+    assert lib.kmpc_strerror(100 + 1).decode() == "optimal_inaccurate"
+
+
+def test_argument_errors_need_no_gpu():
+    lib = _lib.load()
+    d = _lib.SolveDesc()
+    d.B, d.N, d.H = 1, 5, 0
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d.H, d.N = 40, 5
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -2
+    d.H, d.B = 5, 0
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == 0
+
+
+def test_struct_layouts_match_header(tmp_path):
+    prog = tmp_path / "layout.c"
+    prog.write_text(f'''#include <stdio.h>
+#include <stddef.h>
+#include "{HEADER}"
+int main(void) {{
+  printf("%zu %zu %zu %zu\\n", sizeof(kmpc_solve_desc), offsetof(kmpc_solve_desc, tol),
+         offsetof(kmpc_solve_desc, return_full_W), offsetof(kmpc_solve_desc, max_turnover));
+  printf("%zu %zu %zu\\n", sizeof(kmpc_mlp), offsetof(kmpc_mlp, weight), offsetof(kmpc_mlp, bias));
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
+         offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
+         offsetof(kmpc_rollout_desc, std));
+  return 0;
+}}
+''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(prog), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    S, M, R = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc
+    expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
+              ctypes.sizeof(M), M.weight.offset, M.bias.offset,
+              ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset]
+    assert [int(x) for x in out] == expect
+
+
+def test_reference_api_surface():
+    """Field names/defaults of the reference dataclasses (mpc.py:17-25, backtest.py:22-30) and the
+    public signatures the reference's callers use."""
+    c = pkg.MPCConfig()
+    assert (c.horizon, c.gamma, c.cost_coeff, c.max_turnover, c.allow_short, c.solver) == \
+        (5, 0.0, 0.001, 0.2, False, "ECOS")
+    b = pkg.BacktestConfig()
+    assert (b.initial_capital, b.horizon, b.rebalance_freq, b.cost_coeff, b.risk_free_rate, b.allow_short) == \
+        (10000.0, 5, 1, 0.001, 0.0, False)
+    assert list(inspect.signature(pkg.solve_mpc_log_utility).parameters) == \
+        ["current_weights", "predicted_log_returns", "config"]
+    assert list(inspect.signature(pkg.run_backtest).parameters) == ["strategy", "env", "config", "verbose"]
+    assert list(inspect.signature(pkg.KoopmanMPCStrategy.__init__).parameters) == \
+        ["self", "model", "mpc_config", "device"]
+    assert list(inspect.signature(pkg.KoopmanMPCStrategy.rebalance).parameters) == \
+        ["self", "t", "current_weights", "env", "lookback_window"]
+
+
+def test_product_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.KmpcError):
+        pkg.solve_mpc_log_utility(np.array([0.5, 0.5]), np.zeros((1, 2), np.float32), pkg.MPCConfig(horizon=1))
+    with pytest.raises(_lib.KmpcError):
+        pkg.solve_mpc_log_utility_batched(torch.ones(1, 2, dtype=torch.float64) / 2, torch.zeros(1, 1, 2),
+                                          pkg.MPCConfig(horizon=1))

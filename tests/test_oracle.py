@@ -1,0 +1,102 @@
+"""The CPU oracle (oracle/kmpc_oracle.c) pinned against the reference's known answers and
+independent solvers. CPU only."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import dense_ipm, solver
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def feasible(W, wp, tau, short, tol=1e-8):
+    ok = np.allclose(W.sum(-1), 1.0, atol=tol)
+    if not short:
+        ok &= bool((W >= -tol).all())
+    if tau > 0:
+        prev = wp
+        for t in range(W.shape[0]):
+            ok &= np.abs(W[t] - prev).sum() <= tau + tol
+            prev = W[t]
+    return bool(ok)
+
+
+@pytest.mark.parametrize("precision", ["ld", "d"])
+def test_reference_test_mpc_known_answers(precision):
+    """Exact optima of the reference's tests/test_mpc.py cases (lines 25-55)."""
+    k = np.load(os.path.join(GOLD, "mpc_kat.npz"))
+    W, st, obj, _ = solver.solve(k["pref_wp"], k["pref_y"], 0.0, 0.2, precision=precision)
+    assert st == 0 and W.shape == (1, 2)
+    assert np.abs(W - k["pref_W"]).max() < 1e-6          # turnover cap binds at [0.6, 0.4]
+    assert W[0, 0] > 0.5 and W[0, 1] < 0.5              # the reference's assertion
+    W, st, obj, _ = solver.solve(k["cost_wp"], k["cost_y"], 10.0, 0.2, precision=precision)
+    assert st == 0 and np.abs(W - k["cost_W"]).max() < 1e-6
+    # test_mpc_feasibility: flat returns, cost 0 -> any feasible point; constraints must hold
+    W, st, obj, _ = solver.solve(k["feas_wp"], k["feas_y"], 0.0, 0.2, precision=precision)
+    assert st == 0 and W.shape == (3, 5)
+    assert feasible(W, k["feas_wp"], 0.2, False)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mpc_small_*.npz"))))
+def test_oracle_matches_dense_ipm_and_slsqp(path):
+    g = np.load(path)
+    c, tau, short = g["config"]
+    short = bool(short)
+    for b in range(g["W"].shape[0]):
+        W = g["W"][b]
+        assert g["status"][b] == 0
+        assert feasible(W, g["w_prev"][b], tau, short)
+        f = dense_ipm.reference_objective(W, g["w_prev"][b], g["yhat"][b], c)
+        fd = dense_ipm.reference_objective(g["W_dense"][b], g["w_prev"][b], g["yhat"][b], c)
+        fs = dense_ipm.reference_objective(g["W_slsqp"][b], g["w_prev"][b], g["yhat"][b], c)
+        # the oracle is at least as good as both independent solvers (to 1e-9) ...
+        assert f >= max(fd, fs) - 1e-9
+        # ... and agrees with the dense IPM on the optimum value
+        assert abs(f - fd) < 1e-8
+        if c > 0 and not short:
+            # strictly penalised turnover: the optimum is unique in practice; weights agree
+            assert np.abs(W - g["W_dense"][b]).max() < 1e-5
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mpc_cfg*.npz"))))
+def test_oracle_reproduces_goldens_in_both_precisions(path):
+    g = np.load(path)
+    c, tau, short = g["config"]
+    B = min(g["W"].shape[0], 8 if "N500" not in path else 1)
+    for prec in ("ld", "d"):
+        W, st, obj, _ = solver.solve_batch(g["w_prev"][:B], g["yhat"][:B], c, tau, bool(short), precision=prec)
+        assert (st <= 1).all()
+        for b in range(B):
+            assert feasible(W[b], g["w_prev"][b], tau, bool(short), tol=1e-7)
+        if prec == "ld":      # the parity reference reproduces itself
+            assert np.abs(obj - g["obj"][:B]).max() < 1e-9
+            assert np.abs(W[:, 0] - g["W"][:B, 0]).max() < 1e-9
+        else:                 # float64 (the CPU baseline / the device arithmetic): the parity bar
+            assert np.abs(obj - g["obj"][:B]).max() < 1e-6 + 1e-5 * np.abs(g["obj"][:B]).max()
+            assert np.abs(W[:, 0] - g["W"][:B, 0]).max() < 1e-3
+
+
+def test_pure_simplex_closed_form():
+    """cost 0, no cap: log(R.w) on the simplex is maximised at the best asset of each period."""
+    g = np.load(os.path.join(GOLD, "mpc_cfg2_N30_H5_simplex.npz"))
+    for b in range(g["W"].shape[0]):
+        best = np.argmax(g["yhat"][b], axis=-1)
+        expect = np.eye(g["W"].shape[-1])[best]
+        assert np.abs(g["W"][b] - expect).max() < 1e-6
+
+
+def test_status_and_fallback_semantics():
+    """mpc.py:113-115: non-optimal status -> tile(current_weights), value None (NaN here)."""
+    y = np.array([[0.01, 0.0]], np.float32)
+    # infeasible: w_prev off the simplex, turnover cap too tight to reach it
+    W, st, obj, _ = solver.solve([1.0, 1.0], y, 1e-3, 0.2)
+    assert solver.STATUS_NAMES[st] == "infeasible"
+    assert np.array_equal(W, np.array([[1.0, 1.0]])) and np.isnan(obj)
+    # non-finite predictions
+    W, st, obj, _ = solver.solve([0.5, 0.5], np.array([[np.nan, 0.0]], np.float32), 1e-3, 0.2)
+    assert solver.STATUS_NAMES[st] == "solver_error" and np.array_equal(W, [[0.5, 0.5]])
+    # shorting allowed, no cost, no cap: log utility unbounded
+    W, st, obj, _ = solver.solve([0.5, 0.5], y, 0.0, 0.0, allow_short=True)
+    assert solver.STATUS_NAMES[st] == "unbounded" and np.array_equal(W, [[0.5, 0.5]])
