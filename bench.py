@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark: MPC window-solves/sec (BASELINE.json metric) on the C3 workload.
+
+One *window* is one ``KoopmanMPCStrategy.rebalance`` equivalent (reference backtest.py:80-131):
+obs_t [obs] and w_prev [N] -> Koopman rollout yhat [H, N] -> log-utility MPC solve -> W[0].
+One *step* is one pass of that path over the rank's whole batch of synthetic windows, with all
+inputs resident in HBM before the timed region starts:
+
+    yhat = DeviceKoopman.rollout(obs)              (kmpc_rollout: fp32 MFMA GEMM chain)
+    W0, status, value = solve_mpc_log_utility_batched(w_prev, yhat)   (kmpc_solve: f64 IPM)
+    [N > 1] dist.gather(W0 -> rank 0)              (the one RCCL collective)
+
+This is the launch sequence kmpc_window issues; it is split here only so that HIP events can
+bracket the solve kernel alone (the dominant kernel) for the roofline figure.
+
+Workload (BASELINE configs[2]): 65536 windows per GPU, N = 100 assets, latent
+L = 256, H = 10, obs = N * 20 = 2000, the finance_sparse GenericKM layout (encoder
+Linear(2000,1024)-ReLU-Linear(1024,1024)-ReLU-Linear(1024,256), norm 'id', linear decoder without
+bias), K = random orthogonal x 0.95, MPC cost 1e-3, max_turnover 0.2, no short. Weights and inputs
+are synthetic (seeded), as SURVEY §8d prescribes; multi-GPU is weak scaling (65536 windows per
+rank, rank r draws its own seeded block of the global window stream).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MPC window-solves/sec (batched backtest) at 1/2/4/8 MI355X vs host-CPU ref"
+HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--windows", type=int, default=65536, help="windows per GPU per step")
+    p.add_argument("--assets", type=int, default=100)
+    p.add_argument("--latent", type=int, default=256)
+    p.add_argument("--horizon", type=int, default=10)
+    p.add_argument("--emb", type=int, default=20)
+    p.add_argument("--hidden", type=int, default=1024)
+    p.add_argument("--cpu-seconds", type=float, default=20.0,
+                   help="approximate CPU-baseline budget (0 disables the cpu_baseline leg)")
+    return p.parse_args()
+
+
+def make_state_dict(obs: int, L: int, hidden: int, seed: int = 0) -> dict:
+    """finance_sparse GenericKM state_dict layout (config.py:438-467, model.py:701-797)."""
+    g = torch.Generator().manual_seed(seed)
+
+    def linear(n_out, n_in, bias=True):
+        bound = 1.0 / np.sqrt(n_in)      # nn.Linear default init range
+        W = (torch.rand(n_out, n_in, generator=g) * 2 - 1) * bound
+        b = (torch.rand(n_out, generator=g) * 2 - 1) * bound if bias else None
+        return W, b
+
+    sd = {}
+    dims = [obs, hidden, hidden, L]
+    for k in range(3):
+        W, b = linear(dims[k + 1], dims[k])
+        sd[f"encoder.network.{2 * k}.weight"], sd[f"encoder.network.{2 * k}.bias"] = W, b
+    sd["decoder.network.0.weight"] = linear(obs, L, bias=False)[0]
+    q, _ = torch.linalg.qr(torch.randn(L, L, generator=g, dtype=torch.float64))
+    sd["kmat"] = (0.95 * q).float()
+    return sd
+
+
+MODEL_CFG = {"MODEL": {"MODEL_NAME": "GenericKM", "NORM_FN": "id",
+                       "ENCODER": {"ACTIVATION": "relu", "LAST_RELU": False},
+                       "DECODER": {"ACTIVATION": "relu"}}}
+
+
+def make_inputs(B: int, N: int, obs: int, seed: int, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(B, obs, generator=g)                                   # standardized embedding
+    wp = torch.distributions.Dirichlet(torch.ones(N, dtype=torch.float64)).sample((B,))  # uses global RNG
+    return x.to(device), wp.to(device)
+
+
+def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, H, N, cfg, budget_s):
+    """The oracle's CPU restatement (numpy fp32 rollout + OpenMP float64 IPM) timed on a bounded
+    sample of the same windows on this host's cores. Returns (cpu_baseline dict, parity dict)."""
+    from oracle import rollout as orollout, solver as osolver
+    spec = {"kind": "generic",
+            "enc_w": [sd[f"encoder.network.{2 * k}.weight"].numpy() for k in range(3)],
+            "enc_b": [sd[f"encoder.network.{2 * k}.bias"].numpy() for k in range(3)],
+            "enc_act": "relu", "kmat": sd["kmat"].numpy(), "norm_fn": "id",
+            "dec_w": [sd["decoder.network.0.weight"].numpy()], "dec_b": [None]}
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+
+    def run(lo, hi):
+        x = x_gpu[lo:hi].cpu().numpy()
+        wp = wp_gpu[lo:hi].cpu().numpy()
+        t0 = time.perf_counter()
+        y = orollout.rollout(spec, x, H, N, mean, std)
+        W, st, obj, it = osolver.solve_batch(wp, y, cfg.cost_coeff, cfg.max_turnover, cfg.allow_short,
+                                             precision="d")
+        return time.perf_counter() - t0, y, W, st
+
+    dt, _, _, _ = run(0, 2 * cores)                        # calibration (+ warms BLAS / OpenMP)
+    per = dt / (2 * cores)
+    n = int(min(max(budget_s / max(per, 1e-6), 2 * cores), x_gpu.shape[0]))
+    dt, y, W, st = run(0, n)
+    base = {"value": n / dt, "unit": "windows/s", "cores": cores, "kind": "port",
+            "sample": f"first {n} windows of rank 0's C3 batch: numpy fp32 rollout (oracle/rollout.py) + "
+                      f"OpenMP float64 IPM (oracle/kmpc_oracle.c, {cores} threads), {dt:.1f} s"}
+    W0 = W0_gpu[:n].cpu().numpy()
+    ok = st <= 1
+    parity = {"windows": n, "cpu_optimal": int(ok.sum()),
+              "max_abs_dW0_vs_cpu": float(np.abs(W0[ok] - W[ok, 0]).max()) if ok.any() else None}
+    return base, parity
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
+                                                       solve_mpc_log_utility_batched)
+    B, N, L, H = args.windows, args.assets, args.latent, args.horizon
+    obs = N * args.emb
+    sd = make_state_dict(obs, L, args.hidden, seed=0)
+    model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, MODEL_CFG), dev)
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    mean_d = torch.tensor(mean, device=dev)
+    std_d = torch.tensor(std, device=dev)
+    torch.manual_seed(1000 + rank)
+    x, wp = make_inputs(B, N, obs, seed=rank, device=dev)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, allow_short=False)
+    gather_buf = ([torch.empty(B, N, dtype=torch.float64, device=dev) for _ in range(world)]
+                  if (world > 1 and rank == 0) else None)
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(e=None):
+        if e is not None:
+            e[0].record()
+        y = model.rollout(x, mean_d, std_d, H, N)
+        if e is not None:
+            e[1].record()
+        W0, st, val = solve_mpc_log_utility_batched(wp, y, cfg)
+        if e is not None:
+            e[2].record()
+        if world > 1:
+            dist.gather(W0, gather_buf, dst=0)
+        return y, W0, st, val
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        y, W0, st, val = step(ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roll_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    solve_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    st_np = st.cpu().numpy()
+    n_opt = int((st_np <= 1).sum())
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        # algorithmic bytes of one solve launch: read yhat f32 [B,H,N] + w_prev f64 [B,N];
+        # write W0 f64 [B,N] + status i32 + value f64 (+ iters i32) per window
+        solve_bytes = B * (4 * H * N + 8 * N + 8 * N + 4 + 8 + 4)
+        achieved = solve_bytes / (solve_ms * 1e-3)
+        roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
+                                + H * (L * L + L * N))
+        line = {
+            "metric": METRIC, "value": value, "unit": "windows/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 rollout / f64 solve",
+            "data": "synthetic (seeded N(0,1) standardized embeddings, Dirichlet w_prev, random-init finance_sparse weights)",
+            "config": {"workload": f"C3: {B} windows/GPU, {N} assets, latent {L}, H={H}, obs {obs}, "
+                                   f"GenericKM enc [{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
+                       "windows_per_gpu": B, "global_windows_per_step": world * B,
+                       "parallelism": f"windows sharded over {world} GPU(s), RCCL gather of W0"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "traffic": None,
+                         "kernel": "kmpc_solve (solve_kernel)",
+                         "algorithmic_bytes_per_window": solve_bytes // B, "launch_ms": solve_ms},
+            "kernels": {"rollout_ms": roll_ms, "solve_ms": solve_ms,
+                        "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
+                        "rollout_mfma_frac": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK},
+            "solver": {"optimal_or_inaccurate": n_opt, "windows": B},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            base, parity = cpu_baseline(sd, mean, std, x, wp, W0, H, N, cfg, args.cpu_seconds)
+            line["cpu_baseline"] = base
+            line["cpu_parity"] = parity
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

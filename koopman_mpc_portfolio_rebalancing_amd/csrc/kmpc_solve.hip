@@ -29,6 +29,7 @@ constexpr int WAVE = 64;
 constexpr int MAX_WAVES = KMPC_MAX_N / WAVE;   // 16
 constexpr int RED_W = 64;                      // slots per wave in the reduction buffer
 constexpr int PW = 32;                         // Schur entries per Gram panel
+constexpr double REFINE_RTOL = 1e-9;           // refinement stops at ||r|| <= REFINE_RTOL ||b|| (oracle: same)
 
 struct SolveArgs {
     int B, N, H;
@@ -447,6 +448,7 @@ __device__ __forceinline__ void newton(Thread<HM>& T, Shared<HM>& sh, int nw, in
         sh.b6[t] = (t < H) ? -sh.rp[t] : 0.0;
     }
     __syncthreads();
+    double bn = 0.0;   // ||b||_inf of this thread's rows
     {
         double b0[HM], b1[HM];
 #pragma unroll
@@ -457,11 +459,16 @@ __device__ __forceinline__ void newton(Thread<HM>& T, Shared<HM>& sh, int nw, in
                 dual_residual<HM>(T, sh, t, rdw, rds);
                 b0[t] = -rdw;
                 b1[t] = -rds;
+                bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
+                                   fmax(fabs(T.rc1[t]), fmax(fabs(T.rc2[t]), fabs(T.rc3[t])))));
             }
+            if (threadIdx.x == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
         }
         lsolve<HM>(T, sh, b0, b1, true, nw);
     }
     __syncthreads();
+    if (n_refine > 0) bn = block_max1(bn, sh.red, nw);
+    // adaptive refinement: stop once ||r||_inf <= REFINE_RTOL ||b||_inf (block-uniform decision)
     for (int r = 0; r < n_refine; ++r) {
         // residual of rows (1), (2), (6), (7); rows (3)-(5) hold by construction
         {
@@ -498,7 +505,16 @@ __device__ __forceinline__ void newton(Thread<HM>& T, Shared<HM>& sh, int nw, in
             sw[t] = T.dw[t];
             ss[t] = T.ds[t];
         }
-        __syncthreads();
+        {
+            double rn = 0.0;
+#pragma unroll
+            for (int t = 0; t < HM; ++t) {
+                rn = fmax(rn, fmax(fabs(r0[t]), fabs(r1[t])));
+                if (threadIdx.x == 0 && t < H) rn = fmax(rn, fabs(sh.b6[t] - sh.t_sdw[t]));
+            }
+            rn = block_max1(rn, sh.red, nw);
+            if (rn <= REFINE_RTOL * bn) break;
+        }
         if (threadIdx.x == 0) {
 #pragma unroll
             for (int t = 0; t < HM; ++t) {
@@ -1061,7 +1077,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.max_iter = d->max_iter > 0 ? d->max_iter : 80;
     a.tol = d->tol > 0.0 ? d->tol : 1e-11;
     a.return_full = d->return_full_W;
-    a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 2);
+    a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 6);
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
