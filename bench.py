@@ -90,7 +90,7 @@ def make_inputs(B: int, N: int, obs: int, seed: int, device):
     return x.to(device), wp.to(device)
 
 
-def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, H, N, cfg, budget_s):
+def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg, budget_s):
     """The oracle's CPU restatement (numpy fp32 rollout + OpenMP float64 IPM) timed on a bounded
     sample of the same windows on this host's cores. Returns (cpu_baseline dict, parity dict)."""
     from oracle import rollout as orollout, solver as osolver
@@ -117,10 +117,19 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, H, N, cfg, budget_s):
     base = {"value": n / dt, "unit": "windows/s", "cores": cores, "kind": "port",
             "sample": f"first {n} windows of rank 0's C3 batch: numpy fp32 rollout (oracle/rollout.py) + "
                       f"OpenMP float64 IPM (oracle/kmpc_oracle.c, {cores} threads), {dt:.1f} s"}
-    W0 = W0_gpu[:n].cpu().numpy()
-    ok = st <= 1
-    parity = {"windows": n, "cpu_optimal": int(ok.sum()),
-              "max_abs_dW0_vs_cpu": float(np.abs(W0[ok] - W[ok, 0]).max()) if ok.any() else None}
+    # parity on the same inputs: the float64 oracle solve of the device's own yhat (256 windows),
+    # and the rollout (numpy fp32 vs MFMA fp32) relative error over the timed sample
+    k = min(256, n)
+    yg = y_gpu[:k].cpu().numpy()
+    Wo, sto, vo, _ = osolver.solve_batch(wp_gpu[:k].cpu().numpy(), yg, cfg.cost_coeff, cfg.max_turnover,
+                                         cfg.allow_short, precision="d")
+    W0 = W0_gpu[:k].cpu().numpy()
+    vg = val_gpu[:k].cpu().numpy()
+    ynp = y_gpu[:n].cpu().numpy()
+    parity = {"windows": k, "oracle_optimal": int((sto <= 1).sum()),
+              "max_abs_dW0": float(np.abs(W0 - Wo[:, 0]).max()),
+              "max_abs_dobj": float(np.abs(vg - vo).max()), "max_abs_obj": float(np.abs(vo).max()),
+              "rollout_max_rel_err": float(np.abs(ynp - y).max() / np.abs(y).max())}
     return base, parity
 
 
@@ -141,6 +150,7 @@ def main():
 
     from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
                                                        solve_mpc_log_utility_batched)
+    from koopman_mpc_portfolio_rebalancing_amd.shard import gather_rows
     B, N, L, H = args.windows, args.assets, args.latent, args.horizon
     obs = N * args.emb
     sd = make_state_dict(obs, L, args.hidden, seed=0)
@@ -152,8 +162,6 @@ def main():
     torch.manual_seed(1000 + rank)
     x, wp = make_inputs(B, N, obs, seed=rank, device=dev)
     cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, allow_short=False)
-    gather_buf = ([torch.empty(B, N, dtype=torch.float64, device=dev) for _ in range(world)]
-                  if (world > 1 and rank == 0) else None)
 
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
@@ -167,7 +175,7 @@ def main():
         if e is not None:
             e[2].record()
         if world > 1:
-            dist.gather(W0, gather_buf, dst=0)
+            gather_rows(W0, world * B, world, rank, dst=0)
         return y, W0, st, val
 
     for _ in range(args.warmup):
@@ -221,7 +229,7 @@ def main():
             "solver": {"optimal_or_inaccurate": n_opt, "windows": B},
         }
         if world == 1 and args.cpu_seconds > 0:
-            base, parity = cpu_baseline(sd, mean, std, x, wp, W0, H, N, cfg, args.cpu_seconds)
+            base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base
             line["cpu_parity"] = parity
         print(json.dumps(line), flush=True)

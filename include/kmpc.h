@@ -73,7 +73,7 @@ typedef struct kmpc_solve_desc {
     double tol;            /* complementarity tolerance (<= 0 -> default 1e-11)   */
     int    return_full_W;  /* 0: w_out is [B,N] (W[0]); 1: w_out is [B,H,N]       */
     int    n_refine;       /* max iterative-refinement steps per Newton solve; refinement stops once
-                              ||r||_inf <= 1e-9 ||b||_inf (<0 -> none, 0 -> default 6)             */
+                              ||r||_inf <= 1e-7 ||b||_inf (<0 -> none, 0 -> default 3)             */
 } kmpc_solve_desc;
 
 int kmpc_solve(const kmpc_solve_desc* desc,

@@ -29,7 +29,13 @@ constexpr int WAVE = 64;
 constexpr int MAX_WAVES = KMPC_MAX_N / WAVE;   // 16
 constexpr int RED_W = 64;                      // slots per wave in the reduction buffer
 constexpr int PW = 32;                         // Schur entries per Gram panel
-constexpr double REFINE_RTOL = 1e-9;           // refinement stops at ||r|| <= REFINE_RTOL ||b|| (oracle: same)
+#ifdef KMPC_STATS
+__device__ unsigned long long g_stats[2];   // dev builds only: refinement steps, Newton solves
+#endif
+#ifndef KMPC_REFINE_RTOL
+#define KMPC_REFINE_RTOL 1e-7
+#endif
+constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;           // refinement stops at ||r|| <= REFINE_RTOL ||b|| (oracle: same)
 
 struct SolveArgs {
     int B, N, H;
@@ -469,7 +475,8 @@ __device__ __forceinline__ void newton(Thread<HM>& T, Shared<HM>& sh, int nw, in
     __syncthreads();
     if (n_refine > 0) bn = block_max1(bn, sh.red, nw);
     // adaptive refinement: stop once ||r||_inf <= REFINE_RTOL ||b||_inf (block-uniform decision)
-    for (int r = 0; r < n_refine; ++r) {
+    int r = 0;
+    for (; r < n_refine; ++r) {
         // residual of rows (1), (2), (6), (7); rows (3)-(5) hold by construction
         {
             double adw[HM], sds[HM], sdw[HM];
@@ -539,6 +546,11 @@ __device__ __forceinline__ void newton(Thread<HM>& T, Shared<HM>& sh, int nw, in
         }
         __syncthreads();
     }
+#ifdef KMPC_STATS
+    if (threadIdx.x == 0) { atomicAdd(&g_stats[0], (unsigned long long)r); atomicAdd(&g_stats[1], 1ull); }
+#else
+    (void)r;
+#endif
     // dz4 / dl4 of the final direction
     double sds[HM];
 #pragma unroll
@@ -1077,7 +1089,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.max_iter = d->max_iter > 0 ? d->max_iter : 80;
     a.tol = d->tol > 0.0 ? d->tol : 1e-11;
     a.return_full = d->return_full_W;
-    a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 6);
+    a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 3);
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
@@ -1093,3 +1105,15 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
 }
 
 }  // namespace kmpc
+
+#ifdef KMPC_STATS
+extern "C" int kmpc_debug_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmpc::g_stats), sizeof(unsigned long long) * 2) != hipSuccess)
+        return KMPC_ERR_LAUNCH;
+    if (reset) {
+        unsigned long long z[2] = {0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kmpc::g_stats), z, sizeof(z)) != hipSuccess) return KMPC_ERR_LAUNCH;
+    }
+    return KMPC_OK;
+}
+#endif

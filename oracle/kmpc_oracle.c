@@ -32,7 +32,7 @@
  *     the cancellation-free recursion pi_t = W1_t + E_t pi_{t-1} / (pi_{t-1} + E_t)) and
  *     U = [a_t | sqrt(rho_t) D^T e_t]; the budget rows 1'w_t = 1 join U in a 3H x 3H Schur system,
  *   - iterative refinement against the unreduced Newton system, adaptive: refine while
- *     ||r||_inf > 1e-9 ||b||_inf, at most n_refine (6) steps. Near the optimum the Schur system
+ *     ||r||_inf > 1e-7 ||b||_inf, at most n_refine (3) steps. Near the optimum the Schur system
  *     is as ill-conditioned as 1/mu, and a fixed 1-2 steps leave objective errors ~1e-6.
  *
  * Parity of this oracle is pinned in tests/test_oracle.py against the exact optima of the
@@ -371,7 +371,7 @@ static void newton(ws_t* W) {
     lsolve(W, W->b);
     real* sol[7] = {W->dw, W->ds, W->dl1, W->dl2, W->dl3, W->dl4, W->dnu};
     static double adapt = -1;   /* stop refining once ||r||_inf <= adapt ||b||_inf */
-    if (adapt < 0) adapt = getenv("KMPC_ORACLE_REFINE_RTOL") ? atof(getenv("KMPC_ORACLE_REFINE_RTOL")) : 1e-9;
+    if (adapt < 0) adapt = getenv("KMPC_ORACLE_REFINE_RTOL") ? atof(getenv("KMPC_ORACLE_REFINE_RTOL")) : 1e-7;
     real bn = 0;
     if (adapt > 0) {
         for (int j = 0; j < 7; ++j) { size_t n = j < 5 ? HN : (size_t)H; for (size_t k = 0; k < n; ++k) bn = RFMAX(bn, RFABS(W->b[j][k])); }
@@ -484,7 +484,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
     if (finite && ws_init(&W, N, H) == 0) {
         W.N = N; W.H = H; W.K = 3 * H;
         W.hw = !allow_short; W.hs = (c > 0) || (tau > 0); W.ht = tau > 0;
-        W.n_refine = getenv("KMPC_ORACLE_REFINE") ? atoi(getenv("KMPC_ORACLE_REFINE")) : 6;
+        W.n_refine = getenv("KMPC_ORACLE_REFINE") ? atoi(getenv("KMPC_ORACLE_REFINE")) : 3;
         real sig = c;
         for (int i = 0; i < N; ++i) W.wp[i] = wp[i];
         for (size_t k = 0; k < HN; ++k) {
