@@ -26,7 +26,7 @@ def is_stale() -> bool:
     return any(os.path.getmtime(s) > t for s in sources())
 
 
-def build(force: bool = False, jobs: int = 3) -> str:
+def build(force: bool = False, jobs: int = 7) -> str:
     if force:
         subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
     if force or is_stale():

@@ -1,0 +1,25 @@
+// kmpc_solve_args.h — arguments of the batched MPC solve kernel and its per-horizon launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace kmpc {
+
+struct SolveArgs {
+    int B, N, H;
+    double c, tau;
+    int allow_short, max_iter, return_full, n_refine;
+    double tol;
+    const float* yhat;
+    const double* wp;
+    double* wout;
+    int* status;
+    double* obj;
+    int* iters;
+    double* trace;   // debug: per-iteration (mu, rd, pr, step) of problem 0, or null
+};
+
+// ipm_kernel launchers, one translation unit per compile-time horizon bound HM (kmpc_solve_h*.hip)
+template <int HM>
+int launch_ipm(const SolveArgs& a, hipStream_t stream);
+
+}  // namespace kmpc

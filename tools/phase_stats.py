@@ -1,0 +1,37 @@
+"""Dev probe: per-phase s_memtime cycles of the solve kernel (dev builds with -DKMPC_STATS)."""
+import ctypes, glob, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from koopman_mpc_portfolio_rebalancing_amd import _lib, MPCConfig, solve_mpc_log_utility_batched
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+N, H = 100, 10
+rng = np.random.default_rng(0)
+wp = torch.tensor(rng.dirichlet(np.ones(N), B), device="cuda")
+y = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device="cuda")
+from oracle import solver as oracle
+nchk = 64
+Wo, sto, vo, _ = oracle.solve_batch(wp[:nchk].cpu().numpy(), y[:nchk].cpu().numpy(), 1e-3, 0.2, precision="ld")
+names = ["residual+best", "factor:prep", "factor:gram", "factor:chol", "newton", "step+corr", "update", "(lsolve)",
+         "ls:rhs+sinv", "ls:qsolve+bs", "ls:trisolve", "ls:back+sinv", "nt:setup+bn", "nt:lsolve+acc", "nt:resid+max", "nt:tail"]
+libs = sys.argv[2:] or sorted(os.path.basename(p) for p in glob.glob(os.path.join(os.path.dirname(_lib.LIB_PATH), "libkmpc_dev*.so")))
+for name in libs:
+    L = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), name))
+    L.kmpc_debug_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    _lib._lib = L
+    cfg = MPCConfig(horizon=H)
+    solve_mpc_log_utility_batched(wp, y, cfg); torch.cuda.synchronize()
+    st = (ctypes.c_ulonglong * 18)()
+    L.kmpc_debug_stats(st, 1)
+    t = time.time()
+    W, s, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
+    torch.cuda.synchronize(); dt = time.time() - t
+    L.kmpc_debug_stats(st, 1)
+    nb = (B + 255) // 256
+    iters = it.float().mean().item()
+    tot = sum(st[2 + k] for k in range(7))
+    print(f"{name}: {dt*1e3:.1f} ms {B/dt:.0f} win/s iters {iters:.2f} refines/solve {st[0]/max(st[1],1):.3f} "
+          f"status {np.bincount(s.cpu().numpy(), minlength=5)} dobj {np.abs(v[:nchk].cpu().numpy() - vo).max():.2e} "
+          f"dW0 {np.abs(W[:nchk].cpu().numpy() - Wo[:, 0]).max():.2e}")
+    for k in range(16):
+        c = st[2 + k] / nb / iters
+        print(f"   {names[k]:14s} {c:10.0f} cycles/iter  {100*st[2+k]/max(tot,1):5.1f}%")
