@@ -147,6 +147,31 @@ int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc,
                 double*       w_out, int* status, double* obj, int* iters,
                 void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- lock-step backtest bookkeeping for P paths: run_backtest / calculate_metrics ------------ */
+/*
+ * Replaces the per-step body of run_backtest (backtest.py:173-217) for P independent paths run in
+ * lock step (each path's target weights come from kmpc_window / kmpc_solve), and calculate_metrics
+ * (backtest.py:221-249) per path. History layout: hist [P, S, 4] float64 rows
+ * (portfolio_value, return, turnover, cost) — the reference DataFrame columns.
+ */
+typedef struct kmpc_backtest_desc {
+    int    P;            /* paths run in lock step                                   */
+    int    N;            /* assets                                                   */
+    int    S;            /* history rows per path                                    */
+    double cost_coeff;   /* BacktestConfig.cost_coeff (backtest.py:28)               */
+} kmpc_backtest_desc;
+
+/* Step `step` (history row) for every path: cost from the turnover to `target` [P,N] f64, the
+ * realized float32 log-returns of t+1 `realized_next` [P,N] (NULL when t+1 is past the data:
+ * no market move), value [P] and weights [P,N] updated in place (drift with the 1e-8 guard). */
+int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* target,
+                       const float* realized_next, double* weights, double* value, double* hist,
+                       void* stream);
+
+/* metrics [P,5]: Sharpe Ratio, Max Drawdown, Avg Turnover, Final Value, Total Return. */
+int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, double* metrics,
+                          void* stream);
+
 /* Workspace needed by kmpc_rollout / kmpc_solve / kmpc_window (either desc may be NULL). */
 size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc);
 

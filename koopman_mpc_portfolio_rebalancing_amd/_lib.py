@@ -27,7 +27,7 @@ STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbo
                 4: "solver_error"}
 
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
-                    "kmpc_strerror", "kmpc_version")
+                    "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_strerror", "kmpc_version")
 
 
 class KmpcError(RuntimeError):
@@ -56,6 +56,11 @@ class RolloutDesc(ctypes.Structure):
                 ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p)]
 
 
+class BacktestDesc(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int), ("N", ctypes.c_int), ("S", ctypes.c_int),
+                ("cost_coeff", ctypes.c_double)]
+
+
 _lib = None
 
 
@@ -76,6 +81,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_window.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc), vp, vp, vp, vp,
                               vp, vp, vp, vp, sz, vp]
     L.kmpc_window.restype = ctypes.c_int
+    L.kmpc_backtest_step.argtypes = [ctypes.POINTER(BacktestDesc), ctypes.c_int, vp, vp, vp, vp, vp, vp]
+    L.kmpc_backtest_step.restype = ctypes.c_int
+    L.kmpc_backtest_metrics.argtypes = [ctypes.POINTER(BacktestDesc), vp, vp, vp]
+    L.kmpc_backtest_metrics.restype = ctypes.c_int
     L.kmpc_workspace_bytes.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc)]
     L.kmpc_workspace_bytes.restype = ctypes.c_size_t
     L.kmpc_strerror.argtypes = [ctypes.c_int]

@@ -10,6 +10,7 @@ std Sharpe, drawdown, total return relative to the first row).
 """
 from __future__ import annotations
 
+import ctypes
 from abc import ABC, abstractmethod
 from dataclasses import dataclass
 from typing import Any, Dict, Optional, Sequence
@@ -191,3 +192,55 @@ def calculate_metrics(df: pd.DataFrame) -> Dict:
         "Final Value": df["portfolio_value"].iloc[-1],
         "Total Return": (df["portfolio_value"].iloc[-1] / df["portfolio_value"].iloc[0]) - 1.0,
     }
+
+
+METRIC_NAMES = ("Sharpe Ratio", "Max Drawdown", "Avg Turnover", "Final Value", "Total Return")
+
+
+def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
+                          mean, std, n_rows: Optional[int] = None) -> Dict[str, Any]:
+    """P independent backtests of the reference loop (backtest.py:133-219) run in lock step on the
+    device: at every step one batched window launch (kmpc_window over the P
+    paths) and one bookkeeping launch (kmpc_backtest_step); calculate_metrics per path at the end
+    (kmpc_backtest_metrics). Path p reproduces run_backtest on an env whose test rows are obs[p] and
+    whose de-standardized realized log-returns are realized[p].
+
+    Args:
+        obs: [P, T, obs] float32 standardized embeddings (env.test_dataset.data per path).
+        realized: [P, T, N] float32 de-standardized log-returns (the reference's all_returns).
+        mean, std: [N] de-standardisation of the rollout (env.stats).
+        n_rows: len(env.test_dataset) (default T); n_steps = n_rows - config.horizon.
+    Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
+        reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
+    """
+    km = strategy.device_model()
+    dev = km.device
+    x = torch.as_tensor(obs).to(dev, torch.float32).contiguous()
+    r = torch.as_tensor(realized).to(dev, torch.float32).contiguous()
+    if x.dim() != 3 or r.dim() != 3 or x.shape[:2] != r.shape[:2]:
+        raise ValueError("obs must be [P, T, obs] and realized [P, T, N]")
+    P, T, N = r.shape
+    n_rows = T if n_rows is None else int(n_rows)
+    steps = list(range(0, n_rows - config.horizon, config.rebalance_freq))
+    S = len(steps)
+    w = torch.full((P, N), 1.0 / N, dtype=torch.float64, device=dev)       # backtest.py:161
+    value = torch.full((P,), float(config.initial_capital), dtype=torch.float64, device=dev)
+    hist = torch.empty((P, max(S, 1), 4), dtype=torch.float64, device=dev)
+    metrics = torch.empty((P, 5), dtype=torch.float64, device=dev)
+    L = _lib.load()
+    d = _lib.BacktestDesc(P, N, max(S, 1), float(config.cost_coeff))
+    for k, t in enumerate(steps):
+        W0, _, _ = km.window(x[:, t], w, mean, std, N, strategy.mpc_config)
+        rn = r[:, t + 1].contiguous() if t + 1 < T else None
+        with torch.cuda.device(dev):
+            _lib.check(L.kmpc_backtest_step(ctypes.byref(d), k, W0.data_ptr(),
+                                            rn.data_ptr() if rn is not None else None, w.data_ptr(),
+                                            value.data_ptr(), hist.data_ptr(), _lib.stream_handle(dev)))
+    if S:
+        with torch.cuda.device(dev):
+            _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), metrics.data_ptr(),
+                                               _lib.stream_handle(dev)))
+    hist = hist[:, :S]
+    return {"portfolio_value": hist[..., 0], "return": hist[..., 1], "turnover": hist[..., 2],
+            "cost": hist[..., 3], "weights": w,
+            "metrics": {name: metrics[:, j] for j, name in enumerate(METRIC_NAMES)} if S else {}}

@@ -90,3 +90,24 @@ int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc, co
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* target,
+                       const float* realized_next, double* weights, double* value, double* hist,
+                       void* stream) {
+    if (!desc || desc->P < 0 || desc->N < 1 || desc->S < 1 || step < 0 || step >= desc->S)
+        return KMPC_ERR_INVALID;
+    if (desc->P > 0 && (!target || !weights || !value || !hist)) return KMPC_ERR_INVALID;
+    return kmpc::backtest_step_launch(desc, step, target, realized_next, weights, value, hist,
+                                      (hipStream_t)stream);
+}
+
+int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, double* metrics,
+                          void* stream) {
+    if (!desc || desc->P < 0 || desc->S < 0) return KMPC_ERR_INVALID;
+    if (desc->P > 0 && (!hist || !metrics)) return KMPC_ERR_INVALID;
+    return kmpc::backtest_metrics_launch(desc, hist, metrics, (hipStream_t)stream);
+}
+
+}  // extern "C"

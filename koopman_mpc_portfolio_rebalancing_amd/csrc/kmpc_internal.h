@@ -11,6 +11,13 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
                  int* status, double* obj, int* iters, hipStream_t stream,
                  double* trace = nullptr);
 
+// kmpc_backtest.hip
+int backtest_step_launch(const kmpc_backtest_desc* d, int step, const double* target,
+                         const float* realized_next, double* weights, double* value, double* hist,
+                         hipStream_t stream);
+int backtest_metrics_launch(const kmpc_backtest_desc* d, const double* hist, double* metrics,
+                            hipStream_t stream);
+
 // kmpc_rollout.hip
 size_t rollout_workspace_bytes(const kmpc_rollout_desc* d);
 int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, void* ws,

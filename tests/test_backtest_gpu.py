@@ -1,0 +1,123 @@
+"""Lock-step backtest engine on the device: the bookkeeping kernel against
+the numpy restatement of run_backtest (oracle/backtest_ref.py, backtest.py:133-219), the metrics
+kernel against calculate_metrics (backtest.py:221-249), and whole lock-step runs against the
+sequential run_backtest and the reference's recorded run.
+
+Tolerance: the reference computes realized returns as float32 `np.exp(r) - 1` and the device as
+float32 `expf(r) - 1` — the two exp implementations may differ by an ulp of 1.0 (1.2e-7), which
+the subtraction turns into an absolute return difference; returns are therefore compared at
+atol 3e-7 (2.5 float32 ulps of 1.0) and values / turnovers (which see the drifted weights) at
+rtol 1e-6. The first turnover (before any market move) is pure float64 and compared at 1e-14.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from koopman_mpc_portfolio_rebalancing_amd import (BacktestConfig, KoopmanModelSpec, KoopmanMPCStrategy,
+                                                   MPCConfig, run_backtest, run_backtest_lockstep, _lib)
+from koopman_mpc_portfolio_rebalancing_amd.backtest import METRIC_NAMES
+from oracle import backtest_ref
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def device_replay(targets, realized, cost, capital):
+    """kmpc_backtest_step over P paths replaying targets [P, S, N]; realized [P, T, N] (f32)."""
+    P, S, N = targets.shape
+    T = realized.shape[1]
+    L = _lib.load()
+    w = torch.full((P, N), 1.0 / N, dtype=torch.float64, device="cuda")
+    value = torch.full((P,), capital, dtype=torch.float64, device="cuda")
+    hist = torch.empty((P, S, 4), dtype=torch.float64, device="cuda")
+    met = torch.empty((P, 5), dtype=torch.float64, device="cuda")
+    d = _lib.BacktestDesc(P, N, S, cost)
+    r = torch.tensor(realized, device="cuda")
+    tg = torch.tensor(targets, device="cuda")
+    for k in range(S):
+        t = k
+        rn = r[:, t + 1].contiguous() if t + 1 < T else None
+        tk = tg[:, k].contiguous()
+        _lib.check(L.kmpc_backtest_step(ctypes.byref(d), k, tk.data_ptr(), rn.data_ptr() if rn is not None else None,
+                                        w.data_ptr(), value.data_ptr(), hist.data_ptr(), None))
+    _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), met.data_ptr(), None))
+    torch.cuda.synchronize()
+    return hist.cpu().numpy(), met.cpu().numpy()
+
+
+@pytest.mark.parametrize("N,S,tail", [(7, 11, True), (1, 6, False), (300, 8, True)])
+def test_step_kernel_replays_reference_bookkeeping(N, S, tail):
+    """tail: the last step has no t+1 return row (no market move, backtest.py:191)."""
+    rng = np.random.default_rng(N + S)
+    P, capital, cost = 5, 10000.0, 1e-3
+    realized = rng.normal(5e-4, 0.02, (P, S if tail else S + 1, N)).astype(np.float32)
+    targets = rng.dirichlet(np.ones(N), (P, S)) if N > 1 else np.ones((P, S, 1))
+    hist, met = device_replay(targets, realized, cost, capital)
+    for p in range(P):
+        it = iter(targets[p])
+        rows = backtest_ref.run_backtest(lambda t, w: next(it), realized[p], S + 1, 1, N, capital, 1, cost)
+        ref = np.array([[h["portfolio_value"], h["return"], h["turnover"], h["cost"]] for h in rows])
+        np.testing.assert_allclose(hist[p][:, 0], ref[:, 0], rtol=1e-6)
+        np.testing.assert_allclose(hist[p][:, 1], ref[:, 1], rtol=0, atol=3e-7)
+        np.testing.assert_allclose(hist[p][:, 2], ref[:, 2], rtol=1e-6, atol=1e-12)
+        assert hist[p][0, 2] == pytest.approx(ref[0, 2], rel=1e-14)   # before any drift: float64 only
+        np.testing.assert_allclose(hist[p][:, 3], ref[:, 3], rtol=1e-6, atol=1e-12)
+        m = backtest_ref.calculate_metrics(ref[:, 1], ref[:, 2], ref[:, 0])
+        for j, name in enumerate(METRIC_NAMES):
+            assert met[p, j] == pytest.approx(m[name], rel=1e-4, abs=1e-6), name
+
+
+def test_metrics_kernel_matches_calculate_metrics():
+    rng = np.random.default_rng(3)
+    P, S = 9, 40
+    hist = np.empty((P, S, 4))
+    hist[..., 1] = rng.normal(3e-4, 0.01, (P, S))
+    hist[..., 2] = rng.uniform(0, 0.4, (P, S))
+    hist[..., 0] = 1e4 * np.cumprod(1 + hist[..., 1], axis=1)
+    hist[..., 3] = 0.0
+    d = _lib.BacktestDesc(P, 4, S, 1e-3)
+    h = torch.tensor(hist, device="cuda")
+    met = torch.empty((P, 5), dtype=torch.float64, device="cuda")
+    _lib.check(_lib.load().kmpc_backtest_metrics(ctypes.byref(d), h.data_ptr(), met.data_ptr(), None))
+    met = met.cpu().numpy()
+    for p in range(P):
+        m = backtest_ref.calculate_metrics(hist[p, :, 1], hist[p, :, 2], hist[p, :, 0])
+        for j, name in enumerate(METRIC_NAMES):
+            assert met[p, j] == pytest.approx(m[name], rel=1e-12, abs=1e-15), name
+
+
+def test_lockstep_paths_match_sequential_and_reference_runs():
+    from test_backtest_cpu import GoldenEnv
+    g = np.load(os.path.join(GOLD, "backtest_koopman_mpc.npz"))
+    meta = json.loads(str(g["meta"]))
+    sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
+    spec = KoopmanModelSpec.from_state_dict(sd, meta["config"])
+    env = GoldenEnv(g)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(**meta["mpc"]))
+    bcfg = BacktestConfig(**meta["backtest"])
+    data = torch.from_numpy(g["test_data"])
+    realized = env.destandardize_returns(env.extract_current_returns(data))
+    # three paths: the golden env, a time-shuffled copy and a scaled copy of its rows
+    rng = np.random.default_rng(0)
+    perm = torch.from_numpy(rng.permutation(data.shape[0]))
+    obs = torch.stack([data, data[perm], data * 0.5])
+    rets = torch.stack([env.destandardize_returns(env.extract_current_returns(o)) for o in obs])
+    out = run_backtest_lockstep(strat, obs, rets, bcfg, g["mean"], g["std"], n_rows=int(g["test_len"]))
+    val = out["portfolio_value"].cpu().numpy()
+    # path 0 vs the reference's recorded run
+    np.testing.assert_allclose(val[0], g["df_value"], rtol=1e-6)
+    np.testing.assert_allclose(out["turnover"][0].cpu().numpy(), g["df_turnover"], atol=1e-4)
+    assert out["metrics"]["Final Value"][0].item() == pytest.approx(meta["metrics"]["Final Value"], rel=1e-6)
+    # every path vs the sequential run_backtest on an env holding that path's rows
+    for p in range(3):
+        e = GoldenEnv(g)
+        e.test_dataset.data = obs[p].clone()
+        df = run_backtest(strat, e, bcfg, verbose=False)
+        np.testing.assert_allclose(val[p], df["portfolio_value"].values, rtol=1e-6)
+        np.testing.assert_allclose(out["return"][p].cpu().numpy(), df["return"].values, rtol=0, atol=3e-7)
+        # (a turnover of 1e-12 is solver noise around w_prev: absolute floor 1e-6)
+        np.testing.assert_allclose(out["turnover"][p].cpu().numpy(), df["turnover"].values, rtol=1e-6, atol=1e-6)

@@ -42,6 +42,12 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -2
     d.H, d.B = 5, 0
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == 0
+    bt = _lib.BacktestDesc(2, 3, 4, 1e-3)
+    assert lib.kmpc_backtest_step(ctypes.byref(bt), 4, None, None, None, None, None, None) == -1   # step >= S
+    assert lib.kmpc_backtest_step(ctypes.byref(bt), 0, None, None, None, None, None, None) == -1   # null arrays
+    assert lib.kmpc_backtest_metrics(None, None, None, None) == -1
+    bt.P = 0
+    assert lib.kmpc_backtest_metrics(ctypes.byref(bt), None, None, None) == 0
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -56,16 +62,18 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
          offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
          offsetof(kmpc_rollout_desc, std));
+  printf("%zu %zu\\n", sizeof(kmpc_backtest_desc), offsetof(kmpc_backtest_desc, cost_coeff));
   return 0;
 }}
 ''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", str(prog), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    S, M, R = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc
+    S, M, R, Bt = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc, _lib.BacktestDesc
     expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
-              ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset]
+              ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
+              ctypes.sizeof(Bt), Bt.cost_coeff.offset]
     assert [int(x) for x in out] == expect
 
 
