@@ -132,12 +132,23 @@ typedef struct kmpc_rollout_desc {
     kmpc_mlp decoder;
     const float* mean;        /* [N] de-standardisation (data_finance.py:740-742) */
     const float* std;         /* [N] */
+    int obs_ld;               /* row stride of obs in floats (0 -> obs). With obs_ld = N, obs may
+                                 point into a standardized [T, N] return panel: window i reads the
+                                 rows i .. i+d-1 (kmpc_standardize below) — the time-delay
+                                 embedding without materialising it; the first encoder layer's
+                                 column blocks must then be in oldest-lag-first order.          */
 } kmpc_rollout_desc;
 
 int kmpc_rollout(const kmpc_rollout_desc* desc,
                  const float* obs,    /* [B, obs] standardized time-delay embedding */
                  float*       yhat,   /* [B, H, N] */
                  void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- data format before the path: standardize a log-return panel (data_finance.py:243-260, 331) */
+/* z[t, n] = (float)((log_returns[t, n] - mean[n]) / std[n]), float64 arithmetic then float32, as
+ * the reference standardizes in pandas and casts with .astype(np.float32). */
+int kmpc_standardize(int T, int N, const double* log_returns, const double* mean, const double* std,
+                     float* z, void* stream);
 
 /* ---- fused window: rollout -> solve on one stream (KoopmanMPCStrategy.rebalance) ---------- */
 int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc,

@@ -27,7 +27,8 @@ STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbo
                 4: "solver_error"}
 
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
-                    "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_strerror", "kmpc_version")
+                    "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_standardize", "kmpc_strerror",
+                    "kmpc_version")
 
 
 class KmpcError(RuntimeError):
@@ -53,7 +54,7 @@ class RolloutDesc(ctypes.Structure):
                 ("obs", ctypes.c_int), ("model_kind", ctypes.c_int), ("norm_fn", ctypes.c_int),
                 ("encoder", Mlp), ("lista_S", ctypes.c_void_p), ("lista_loops", ctypes.c_int),
                 ("lista_thresh", ctypes.c_float), ("kmat", ctypes.c_void_p), ("decoder", Mlp),
-                ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p)]
+                ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p), ("obs_ld", ctypes.c_int)]
 
 
 class BacktestDesc(ctypes.Structure):
@@ -85,6 +86,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_backtest_step.restype = ctypes.c_int
     L.kmpc_backtest_metrics.argtypes = [ctypes.POINTER(BacktestDesc), vp, vp, vp]
     L.kmpc_backtest_metrics.restype = ctypes.c_int
+    L.kmpc_standardize.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp]
+    L.kmpc_standardize.restype = ctypes.c_int
     L.kmpc_workspace_bytes.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc)]
     L.kmpc_workspace_bytes.restype = ctypes.c_size_t
     L.kmpc_strerror.argtypes = [ctypes.c_int]

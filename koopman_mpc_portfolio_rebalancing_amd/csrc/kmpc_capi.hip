@@ -103,6 +103,13 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
                                       (hipStream_t)stream);
 }
 
+int kmpc_standardize(int T, int N, const double* log_returns, const double* mean, const double* std,
+                     float* z, void* stream) {
+    if (T < 0 || N < 1) return KMPC_ERR_INVALID;
+    if ((size_t)T * N > 0 && (!log_returns || !mean || !std || !z)) return KMPC_ERR_INVALID;
+    return kmpc::standardize_launch(T, N, log_returns, mean, std, z, (hipStream_t)stream);
+}
+
 int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, double* metrics,
                           void* stream) {
     if (!desc || desc->P < 0 || desc->S < 0) return KMPC_ERR_INVALID;

@@ -22,5 +22,7 @@ int backtest_metrics_launch(const kmpc_backtest_desc* d, const double* hist, dou
 size_t rollout_workspace_bytes(const kmpc_rollout_desc* d);
 int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, void* ws,
                    size_t ws_bytes, hipStream_t stream);
+int standardize_launch(int T, int N, const double* y, const double* mean, const double* stdv, float* z,
+                       hipStream_t stream);
 
 }  // namespace kmpc

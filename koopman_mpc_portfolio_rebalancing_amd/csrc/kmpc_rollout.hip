@@ -259,8 +259,10 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (d->decoder.dims[0] != d->L || d->decoder.dims[d->decoder.n_layers] < d->N) return KMPC_ERR_INVALID;
     if (d->model_kind == KMPC_MODEL_LISTA && !d->lista_S) return KMPC_ERR_INVALID;
     if (ws_bytes < rollout_workspace_bytes(d) || (!ws && ws_bytes)) return KMPC_ERR_WORKSPACE;
+    if (d->obs_ld < 0 || (d->obs_ld > 0 && d->obs_ld < d->N)) return KMPC_ERR_INVALID;
     if (d->B == 0) return KMPC_OK;
     const int Bn = d->B, L = d->L, N = d->N, H = d->H;
+    const int obs_ld = d->obs_ld > 0 ? d->obs_ld : d->obs;
     int wmax = L;
     {
         const int we = max_width(d->encoder), wd = max_width(d->decoder);
@@ -283,13 +285,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
 
     // ---- encode ----
     if (d->model_kind == KMPC_MODEL_GENERIC) {
-        rc = run_mlp(d->encoder, Bn, obs, d->obs, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
         if (rc) return rc;
         if (d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, z0, Bn, L);
     } else {
         // c = We(x) (z1 holds c), z = shrink(c); loops: z = shrink(z S + c)   (model.py:200-209)
-        rc = run_mlp(d->encoder, Bn, obs, d->obs, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
         if (rc) return rc;
         const size_t n = (size_t)Bn * L;
         hipLaunchKernelGGL(shrink_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z1, z0, n,
@@ -320,6 +322,24 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         if (rc) return rc;
         float* t = zc; zc = zn; zn = t;
     }
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+// z = f32((y - mean) / std): float64 arithmetic, one rounding to float32 (data_finance.py:243-260, 331)
+__global__ void standardize_kernel(int T, int N, const double* y, const double* mean, const double* stdv,
+                                   float* z) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)T * N) return;
+    const int n = (int)(i % N);
+    z[i] = (float)((y[i] - mean[n]) / stdv[n]);
+}
+
+int standardize_launch(int T, int N, const double* y, const double* mean, const double* stdv, float* z,
+                       hipStream_t s) {
+    const size_t n = (size_t)T * N;
+    if (n == 0) return KMPC_OK;
+    hipLaunchKernelGGL(standardize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, T, N, y, mean,
+                       stdv, z);
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 

@@ -151,13 +151,15 @@ class DeviceKoopman:
         m.last_relu = int(bool(last_relu))
         return m
 
-    def rollout_desc(self, B: int, H: int, N: int, mean: torch.Tensor, std: torch.Tensor) -> _lib.RolloutDesc:
+    def rollout_desc(self, B: int, H: int, N: int, mean: torch.Tensor, std: torch.Tensor,
+                     enc=None, obs_ld: int = 0) -> _lib.RolloutDesc:
         d = _lib.RolloutDesc()
         d.B, d.N, d.H, d.L, d.obs = int(B), int(N), int(H), self.latent, self.obs_size
         s = self.spec
         d.model_kind = _lib.MODEL_LISTA if s.kind == "lista" else _lib.MODEL_GENERIC
         d.norm_fn = _lib.NORM[s.norm_fn]
-        d.encoder = self._mlp(self.enc, s.enc_act, s.enc_last_relu)
+        d.encoder = self._mlp(enc if enc is not None else self.enc, s.enc_act, s.enc_last_relu)
+        d.obs_ld = int(obs_ld)
         d.lista_S = self.S.data_ptr() if self.S is not None else None
         d.lista_loops = int(s.lista_loops)
         d.lista_thresh = float(s.lista_thresh)
@@ -196,6 +198,44 @@ class DeviceKoopman:
         _lib.check(rc)
         return y
 
+    # -- panel mode: the time-delay embedding read in place from a standardized [T, N] panel --
+    def _panel_encoder(self, emb_dim: int, n_assets: int):
+        """First encoder layer with its lag blocks reversed (oldest lag first), so that window i
+        of the embedded matrix (data_finance.py:262-300: [y_t, y_{t-1}, ..., y_{t-d+1}]) is the
+        contiguous panel slice rows i .. i+d-1 (cached per (d, N))."""
+        key = (int(emb_dim), int(n_assets))
+        if getattr(self, "_panel", None) is None:
+            self._panel = {}
+        if key not in self._panel:
+            W0, b0 = self.enc[0]
+            if W0.shape[1] != emb_dim * n_assets:
+                raise ValueError(f"encoder input {W0.shape[1]} != emb_dim * n_assets = {emb_dim * n_assets}")
+            Wr = W0.reshape(W0.shape[0], emb_dim, n_assets).flip(1).reshape(W0.shape[0], -1).contiguous()
+            self._panel[key] = [(Wr, b0)] + list(self.enc[1:])
+        return self._panel[key]
+
+    def rollout_panel(self, z: torch.Tensor, emb_dim: int, first: int, n_windows: int, mean, std,
+                      horizon: int, n_assets: int) -> torch.Tensor:
+        """yhat [n_windows, H, N] for embedded windows first .. first+n_windows-1 of the standardized
+        return panel z [T, N] float32 (kmpc_standardize), without materialising the embedding."""
+        _lib.require_gpu(z)
+        z = z.to(self.device, torch.float32).contiguous()
+        T, N = z.shape
+        if N != n_assets or first < 0 or first + n_windows + emb_dim - 1 > T:
+            raise ValueError("panel window range out of bounds")
+        enc = self._panel_encoder(emb_dim, n_assets)
+        m, s = self._stats(mean, std, n_assets)
+        y = torch.empty((n_windows, horizon, n_assets), dtype=torch.float32, device=self.device)
+        d = self.rollout_desc(n_windows, horizon, n_assets, m, s, enc=enc, obs_ld=N)
+        L = _lib.load()
+        nbytes = L.kmpc_workspace_bytes(ctypes.byref(d), None)
+        ws = self._workspace(nbytes)
+        with torch.cuda.device(self.device):
+            rc = L.kmpc_rollout(ctypes.byref(d), z[first].data_ptr(), y.data_ptr(), ws.data_ptr(), nbytes,
+                                _lib.stream_handle(self.device))
+        _lib.check(rc)
+        return y
+
     def window(self, obs: torch.Tensor, w_prev: torch.Tensor, mean, std, n_assets: int, mpc_config,
                keep_yhat: bool = False, return_full: bool = False):
         """Fused window (kmpc_window): obs [B, obs], w_prev [B, N] -> (W0 or W, status, value[, yhat])."""
@@ -222,3 +262,18 @@ class DeviceKoopman:
                                _lib.stream_handle(self.device))
         _lib.check(rc)
         return (W, status, value, y) if keep_yhat else (W, status, value)
+
+
+def standardize_panel(log_returns, mean, std, device=None) -> torch.Tensor:
+    """z [T, N] float32 = ((y - mean) / std) in float64, cast once — the reference's
+    standardize_returns + .astype(np.float32) (data_finance.py:243-260, 331) — on the device."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    y = torch.as_tensor(log_returns, dtype=torch.float64).to(dev).contiguous()
+    m = torch.as_tensor(np.asarray(mean, np.float64)).to(dev).contiguous()
+    s = torch.as_tensor(np.asarray(std, np.float64)).to(dev).contiguous()
+    T, N = y.shape
+    z = torch.empty((T, N), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.load().kmpc_standardize(T, N, y.data_ptr(), m.data_ptr(), s.data_ptr(), z.data_ptr(),
+                                                _lib.stream_handle(dev)))
+    return z

@@ -102,3 +102,23 @@ def rollout(spec, obs, H, n_assets, mean, std):
             p = (z @ lista_decoder_weight(spec["dict"]).T).astype(np.float32)
         out[:, k, :] = p[:, :n_assets] * std + mean
     return out
+
+
+def standardize(log_returns, mean, std):
+    """data_finance.py:243-260 then .astype(np.float32) (data_finance.py:331): float64 arithmetic,
+    one cast to float32."""
+    y = np.asarray(log_returns, np.float64)
+    return ((y - np.asarray(mean, np.float64)) / np.asarray(std, np.float64)).astype(np.float32)
+
+
+def time_delay_embedding(data, embedding_dim):
+    """data_finance.py:262-300: row i = [y_{i+d-1}, y_{i+d-2}, ..., y_i] (most recent first)."""
+    data = np.asarray(data)
+    T, n = data.shape
+    if T < embedding_dim:
+        raise ValueError("series shorter than the embedding")
+    rows = T - embedding_dim + 1
+    out = np.empty((rows, embedding_dim * n), data.dtype)
+    for j in range(embedding_dim):
+        out[:, j * n:(j + 1) * n] = data[embedding_dim - 1 - j: embedding_dim - 1 - j + rows]
+    return out

@@ -289,8 +289,25 @@ def make_backtest_goldens():
     print("mock", len(dfm))
 
 
+def make_embedding_goldens():
+    """reference standardize_returns + time_delay_embedding (data_finance.py:243-300, 331)."""
+    rng = np.random.default_rng(77)
+    T, N, d = 40, 6, 4
+    y = rng.normal(4e-4, 0.02, (T, N))
+    df = pd.DataFrame(y, columns=[f"A{i}" for i in range(N)],
+                      index=pd.date_range("2020-01-01", periods=T))
+    stats = ref_data.compute_standardization_stats(df, "2020-01-25")
+    z = ref_data.standardize_returns(df, stats).values.astype(np.float32)
+    emb = ref_data.time_delay_embedding(z, d)
+    np.savez_compressed(os.path.join(HERE, "embedding.npz"), log_returns=y, mean=stats.mean, std=stats.std,
+                        standardized=z, embedded=emb, emb_dim=d)
+    print("embedding", emb.shape)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["rollout", "mpc", "backtest"]
+    which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding"]
+    if "embedding" in which:
+        make_embedding_goldens()
     if "rollout" in which:
         make_rollout_goldens()
     if "mpc" in which:

@@ -62,6 +62,7 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
          offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
          offsetof(kmpc_rollout_desc, std));
+  printf("%zu\\n", offsetof(kmpc_rollout_desc, obs_ld));
   printf("%zu %zu\\n", sizeof(kmpc_backtest_desc), offsetof(kmpc_backtest_desc, cost_coeff));
   return 0;
 }}
@@ -73,6 +74,7 @@ int main(void) {{
     expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
               ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
+              R.obs_ld.offset,
               ctypes.sizeof(Bt), Bt.cost_coeff.offset]
     assert [int(x) for x in out] == expect
 

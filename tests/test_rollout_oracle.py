@@ -48,3 +48,11 @@ def test_rollout_restatement_matches_reference(path):
     assert y.shape == ref.shape
     # float32 path, different summation order only
     assert np.abs(y - ref).max() <= 2e-5 * max(scale, 1e-3)
+
+
+def test_embedding_restatement_matches_reference():
+    """oracle standardize + time_delay_embedding == the reference's (data_finance.py:243-300, 331), bit for bit."""
+    g = np.load(os.path.join(GOLD, "embedding.npz"))
+    z = R.standardize(g["log_returns"], g["mean"], g["std"])
+    assert np.array_equal(z, g["standardized"])
+    assert np.array_equal(R.time_delay_embedding(z, int(g["emb_dim"])), g["embedded"])
