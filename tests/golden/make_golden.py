@@ -289,6 +289,34 @@ def make_backtest_goldens():
     print("mock", len(dfm))
 
 
+def make_dmd_goldens():
+    """reference DMDStrategy (baselines.py:127-187): fitted operator and the predicted log-returns
+    it hands to the solver at each call (the solve routed to the oracle, recorded)."""
+    import baselines as ref_baselines
+    N, d, H = 5, 4, 3
+    env = make_env(N, d, 160, seed=5, seq_len=10)
+    calls = []
+
+    def recording_solve(current_weights, predicted_log_returns, config):
+        W, info = oracle_solve(current_weights, predicted_log_returns, config)
+        calls.append((np.array(current_weights, np.float64), np.array(predicted_log_returns, np.float32),
+                      np.array(W, np.float64)))
+        return W, info
+
+    ref_baselines.solve_mpc_log_utility = recording_solve
+    mcfg = ref_mpc.MPCConfig(horizon=H, gamma=0.0, cost_coeff=1e-3, max_turnover=0.3)
+    strat = ref_baselines.DMDStrategy(env.train_dataset.data, mcfg)
+    w = np.ones(N) / N
+    for t in range(12):
+        w = strat.rebalance(t, w, env)
+    np.savez_compressed(os.path.join(HERE, "dmd.npz"), K=strat.K, train_data=env.train_dataset.data.numpy(),
+                        test_data=env.test_dataset.data.numpy(), mean=env.stats.mean, std=env.stats.std,
+                        call_wprev=np.stack([c[0] for c in calls]), call_yhat=np.stack([c[1] for c in calls]),
+                        call_W=np.stack([c[2] for c in calls]), meta=json.dumps({"N": N, "d": d, "H": H,
+                        "mpc": {"horizon": H, "cost_coeff": 1e-3, "max_turnover": 0.3}}))
+    print("dmd", strat.K.shape, len(calls))
+
+
 def make_embedding_goldens():
     """reference standardize_returns + time_delay_embedding (data_finance.py:243-300, 331)."""
     rng = np.random.default_rng(77)
@@ -305,7 +333,9 @@ def make_embedding_goldens():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding"]
+    which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding", "dmd"]
+    if "dmd" in which:
+        make_dmd_goldens()
     if "embedding" in which:
         make_embedding_goldens()
     if "rollout" in which:
