@@ -107,7 +107,7 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
         t0 = time.perf_counter()
         y = orollout.rollout(spec, x, H, N, mean, std)
         W, st, obj, it = osolver.solve_batch(wp, y, cfg.cost_coeff, cfg.max_turnover, cfg.allow_short,
-                                             precision="d")
+                                             max_iter=cfg.max_iter, tol=cfg.tol, precision="d")
         return time.perf_counter() - t0, y, W, st
 
     dt, _, _, _ = run(0, 2 * cores)                        # calibration (+ warms BLAS / OpenMP)
@@ -122,7 +122,7 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
     k = min(256, n)
     yg = y_gpu[:k].cpu().numpy()
     Wo, sto, vo, _ = osolver.solve_batch(wp_gpu[:k].cpu().numpy(), yg, cfg.cost_coeff, cfg.max_turnover,
-                                         cfg.allow_short, precision="d")
+                                         cfg.allow_short, precision="ld")
     W0 = W0_gpu[:k].cpu().numpy()
     vg = val_gpu[:k].cpu().numpy()
     ynp = y_gpu[:n].cpu().numpy()

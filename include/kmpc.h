@@ -70,7 +70,7 @@ typedef struct kmpc_solve_desc {
     double max_turnover;   /* MPCConfig.max_turnover (mpc.py:23); <= 0 disables   */
     int    allow_short;    /* MPCConfig.allow_short  (mpc.py:24)                  */
     int    max_iter;       /* interior-point iteration cap (0 -> default 80)      */
-    double tol;            /* complementarity tolerance (<= 0 -> default 1e-11)   */
+    double tol;            /* complementarity tolerance (<= 0 -> default 1e-9)    */
     int    return_full_W;  /* 0: w_out is [B,N] (W[0]); 1: w_out is [B,H,N]       */
     int    n_refine;       /* max iterative-refinement steps per Newton solve; refinement stops once
                               ||r||_inf <= 1e-7 ||b||_inf (<0 -> none, 0 -> default 3)             */

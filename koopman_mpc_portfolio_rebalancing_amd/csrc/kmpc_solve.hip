@@ -14,7 +14,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.tau = d->max_turnover > 0.0 ? d->max_turnover : 0.0;
     a.allow_short = d->allow_short;
     a.max_iter = d->max_iter > 0 ? d->max_iter : 80;
-    a.tol = d->tol > 0.0 ? d->tol : 1e-11;
+    a.tol = d->tol > 0.0 ? d->tol : 1e-9;
     a.return_full = d->return_full_W;
     a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 3);
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;

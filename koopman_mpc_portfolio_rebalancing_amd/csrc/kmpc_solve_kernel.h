@@ -1124,7 +1124,9 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 // ---- predictor (pass 0) and corrector (pass 1) share one Newton body ----
                 double step = 0.0;
                 for (int pass = 0; pass < 2; ++pass) {
-                    newton<HM, NWM>(T, sh, R, args.n_refine);
+                    // predictor unrefined (it only sets the step estimate, sigma and the
+                    // second-order term), corrector refined adaptively — as the oracle
+                    newton<HM, NWM>(T, sh, R, pass == 0 ? 0 : args.n_refine);
                     KMPC_PH(ph, 4);
                     const double amax = max_step<HM, NWM>(T, sh, R);
                     if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }

@@ -31,7 +31,7 @@ class MPCConfig:
     solver: str = "ECOS"  # accepted for compatibility; the gfx950 interior-point kernel solves
     # extra (defaulted) knobs of the device solver
     max_iter: int = 80
-    tol: float = 1e-11
+    tol: float = 1e-9
     n_refine: int = 0  # 0 -> kernel default
 
 
@@ -42,7 +42,7 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     d.max_turnover = float(config.max_turnover)
     d.allow_short = int(bool(config.allow_short))
     d.max_iter = int(getattr(config, "max_iter", 80))
-    d.tol = float(getattr(config, "tol", 1e-11))
+    d.tol = float(getattr(config, "tol", 1e-9))
     d.return_full_W = int(bool(full))
     d.n_refine = int(getattr(config, "n_refine", 0))
     return d

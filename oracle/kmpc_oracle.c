@@ -580,8 +580,14 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
             }
             if (mu < tol && rd < 10 * tol && pr < 10 * tol) break;
             if (factor(&W) != 0) break;
-            /* predictor: rc = z l */
-            newton(&W);
+            /* predictor: rc = z l (no refinement: the affine direction only sets the step
+               estimate, sigma and the second-order term; the corrector is refined) */
+            {
+                const int nr = W.n_refine;
+                W.n_refine = 0;
+                newton(&W);
+                W.n_refine = nr;
+            }
             real ap = RFMIN(1, max_step(&W));
             real sg = complementarity(&W, ap) / ncon / mu;
             sg = sg * sg * sg;
