@@ -20,7 +20,7 @@ def rows(db, q):
 def main():
     out, trace, pmcs = sys.argv[1], sys.argv[2], sys.argv[3:]
     lines = [f"# rocprofv3 summary ({trace})", "", "## Kernel durations (rocprofv3 --kernel-trace --stats)", "",
-             "| kernel | calls | total ns | average ns | % |", "|---|---|---|---|---|"]
+             "| kernel | calls | total µs | average µs | % |", "|---|---|---|---|---|"]
     for name, calls, tot, avg, pct in rows(trace, "select name,total_calls,total_duration,average,percentage from top_kernels"):
         lines.append(f"| `{name[:90]}` | {calls} | {tot:.0f} | {avg:.0f} | {pct:.2f} |")
     lines += ["", "## Launch resources", "", "| kernel | grid | workgroup | LDS B | scratch B | arch VGPR | accum VGPR | SGPR |",
