@@ -183,6 +183,45 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
 int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, double* metrics,
                           void* stream);
 
+/* ---- mean-variance MPC: replaces solve_mpc_mean_variance (mpc.py:119-184) ------------------ */
+/*
+ * For each problem b:
+ *   maximize_W  sum_t [ w_t . mu_t - gamma w_t' Sigma w_t ] - c sum_t ||w_t - w_{t-1}||_1
+ *   s.t.        1' w_t = 1;  w_t >= 0 unless allow_short  (mpc.py:145-169; no turnover cap)
+ * with w_{-1} = w_prev. mu [B,H,N] float64 (the reference passes predicted log-returns / the
+ * Markowitz rolling mean as mu), Sigma [B,N,N] float64 (sigma_stride = N*N) or one shared [N,N]
+ * (sigma_stride = 0). Outputs as kmpc_solve; failure fallback tile(w_prev), obj = NaN
+ * (mpc.py:180-181). Shapes: H*N <= KMPC_MV_MAX_HN, H <= KMPC_MV_MAX_H.
+ */
+#define KMPC_MV_MAX_HN 128
+#define KMPC_MV_MAX_H  16
+typedef struct kmpc_mv_desc {
+    int    B, N, H;
+    double gamma;          /* MPCConfig.gamma (risk aversion, mpc.py:20)        */
+    double cost_coeff;     /* MPCConfig.cost_coeff                              */
+    int    allow_short;    /* MPCConfig.allow_short                             */
+    int    max_iter;       /* interior-point iteration cap (0 -> 100)           */
+    double tol;            /* complementarity tolerance (<= 0 -> 1e-10)         */
+    int    return_full_W;  /* 0: w_out [B,N] (W[0]); 1: [B,H,N]                  */
+} kmpc_mv_desc;
+
+int kmpc_solve_mv(const kmpc_mv_desc* desc,
+                  const double* mu,        /* [B,H,N] */
+                  const double* sigma,     /* [B,N,N] or [N,N] */
+                  size_t sigma_stride,     /* elements between windows' Sigma (0: shared) */
+                  const double* w_prev,    /* [B,N] */
+                  double* w_out, int* status, double* obj, int* iters, void* stream);
+
+/* ---- Markowitz rolling moments: MarkowitzStrategy.rebalance (baselines.py:70-88) ------------ */
+/* For window b at test row t = ts[b]: returns r_s = z_s * std + mean (float32, as
+ * destandardize_returns, data_finance.py:740-742) of the standardized rows z [T, ldz] (first N
+ * columns = extract_current_returns), s in the last `lookback` rows of [0, t]; mu[b] = mean
+ * (rounded to float32 as the reference's float32 np.mean), sigma[b] = np.cov (ddof 1, float64)
+ * + 1e-6 I; valid[b] = 1 when t + 1 >= 5 (else the strategy holds its weights). */
+int kmpc_rolling_moments(int B, int T, int N, int lookback, const float* z, int ldz,
+                         const float* mean, const float* std, const int* ts,
+                         double* mu, double* sigma, int* valid, void* stream);
+
 /* Workspace needed by kmpc_rollout / kmpc_solve / kmpc_window (either desc may be NULL). */
 size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc);
 

@@ -26,9 +26,12 @@ NORM = {"id": 0, "ball": 1}
 STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
                 4: "solver_error"}
 
+KMPC_MV_MAX_HN = 128     # mean-variance solve: H * N per workgroup
+KMPC_MV_MAX_H = 16
+
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
                     "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_standardize", "kmpc_strerror",
-                    "kmpc_version")
+                    "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments")
 
 
 class KmpcError(RuntimeError):
@@ -40,6 +43,13 @@ class SolveDesc(ctypes.Structure):
                 ("cost_coeff", ctypes.c_double), ("max_turnover", ctypes.c_double),
                 ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
                 ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int), ("n_refine", ctypes.c_int)]
+
+
+class MvDesc(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_int),
+                ("gamma", ctypes.c_double), ("cost_coeff", ctypes.c_double),
+                ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
+                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int)]
 
 
 class Mlp(ctypes.Structure):
@@ -88,6 +98,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_backtest_metrics.restype = ctypes.c_int
     L.kmpc_standardize.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp]
     L.kmpc_standardize.restype = ctypes.c_int
+    L.kmpc_solve_mv.argtypes = [ctypes.POINTER(MvDesc), vp, vp, sz, vp, vp, vp, vp, vp, vp]
+    L.kmpc_solve_mv.restype = ctypes.c_int
+    ci = ctypes.c_int
+    L.kmpc_rolling_moments.argtypes = [ci, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.kmpc_rolling_moments.restype = ctypes.c_int
     L.kmpc_workspace_bytes.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc)]
     L.kmpc_workspace_bytes.restype = ctypes.c_size_t
     L.kmpc_strerror.argtypes = [ctypes.c_int]

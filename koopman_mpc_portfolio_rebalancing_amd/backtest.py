@@ -53,6 +53,16 @@ class BuyAndHoldStrategy(Strategy):
         return current_weights
 
 
+def _cache_key(data):
+    """Key of a device copy of env data: the object itself (kept alive, so its identity cannot be
+    reused by a new object) and, for tensors, the in-place version counter."""
+    return (data, getattr(data, "_version", None))
+
+
+def _cache_hit(key, data) -> bool:
+    return key is not None and key[0] is data and key[1] == getattr(data, "_version", None)
+
+
 def _env_stats(env) -> Optional[tuple]:
     stats = getattr(env, "stats", None)
     mean = getattr(stats, "mean", None)
@@ -107,9 +117,8 @@ class KoopmanMPCStrategy(Strategy):
 
     def _test_data(self, env) -> torch.Tensor:
         data = env.test_dataset.data
-        key = id(data)
-        if self._env_cache[0] != key:
-            self._env_cache = (key, torch.as_tensor(data).to(self._device(), torch.float32).contiguous())
+        if not _cache_hit(self._env_cache[0], data):
+            self._env_cache = (_cache_key(data), torch.as_tensor(data).to(self._device(), torch.float32).contiguous())
         return self._env_cache[1]
 
     # -- windows --------------------------------------------------------------------------------

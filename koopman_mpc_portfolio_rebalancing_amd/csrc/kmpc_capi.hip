@@ -118,3 +118,28 @@ int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, do
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int kmpc_solve_mv(const kmpc_mv_desc* desc, const double* mu, const double* sigma, size_t sigma_stride,
+                  const double* w_prev, double* w_out, int* status, double* obj, int* iters,
+                  void* stream) {
+    if (!desc || desc->B < 0 || desc->N < 1 || desc->H < 1) return KMPC_ERR_INVALID;
+    if (desc->H > KMPC_MV_MAX_H || desc->N * desc->H > KMPC_MV_MAX_HN) return KMPC_ERR_UNSUPPORTED;
+    if (desc->B == 0) return KMPC_OK;
+    if (!mu || !sigma || !w_prev || !w_out || !status || !obj) return KMPC_ERR_INVALID;
+    return kmpc::mv_solve_launch(desc, mu, sigma, sigma_stride, w_prev, w_out, status, obj, iters,
+                                 (hipStream_t)stream);
+}
+
+int kmpc_rolling_moments(int B, int T, int N, int lookback, const float* z, int ldz,
+                         const float* mean, const float* std, const int* ts,
+                         double* mu, double* sigma, int* valid, void* stream) {
+    if (B < 0 || T < 0 || N < 1 || lookback < 1 || ldz < N) return KMPC_ERR_INVALID;
+    if (B == 0) return KMPC_OK;
+    if (!z || !mean || !std || !ts || !mu || !sigma || !valid) return KMPC_ERR_INVALID;
+    return kmpc::rolling_moments_launch(B, T, N, lookback, z, ldz, mean, std, ts, mu, sigma, valid,
+                                        (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -55,6 +55,14 @@ constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
 
 // C = epi(A . B^T). Each lane of an MFMA consumes 16 contiguous k (k = 16h + s, h = lane >> 5),
 // so operand fragments are two ds_read_b128 per row; the k permutation is the same for A and B.
+// y * std + mean with two float32 roundings, as the reference's torch mul then add
+// (data_finance.py:742): FMA contraction off here so yhat matches it bit for bit.
+__device__ __forceinline__ float destandardize(float y, float sd, float mu) {
+#pragma clang fp contract(off)
+    const float p = y * sd;
+    return p + mu;
+}
+
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     __shared__ float As[BM * LDS_STRIDE];
     __shared__ float Bs[BN * LDS_STRIDE];
@@ -141,7 +149,7 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
                     const float av = fabsf(v) - g.thr;
                     v = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
                 } else if (g.epi == EPI_DESTD) {
-                    v = v * sd + mu;
+                    v = destandardize(v, sd, mu);
                 }
                 g.C[(size_t)m * g.ldc + n] = v;
             }

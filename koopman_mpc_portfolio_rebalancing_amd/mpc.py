@@ -6,7 +6,8 @@ raised; a status outside {"optimal", "optimal_inaccurate"} returns ``tile(curren
 ``{"status": s, "value": None}`` (mpc.py:113-115).
 
 ``solve_mpc_log_utility_batched`` is the batched entry point (torch device tensors in and out)
-that the strategies and the benchmark use.
+that the strategies and the benchmark use. ``solve_mpc_mean_variance`` (mpc.py:119-184) and its
+batched form run the mean-variance QP kernel (kmpc_solve_mv) with the same conventions.
 """
 from __future__ import annotations
 
@@ -118,3 +119,93 @@ def solve_mpc_log_utility(
     if st not in ("optimal", "optimal_inaccurate"):
         return np.tile(np.asarray(current_weights, dtype=np.float64), (H, 1)), {"status": st, "value": None}
     return W_np, {"status": st, "value": float(value.item())}
+
+
+# ---- mean-variance MPC (mpc.py:119-184) ------------------------------------------------------
+
+def solve_mpc_mean_variance_batched(
+    current_weights: torch.Tensor,
+    mu: torch.Tensor,
+    cov_matrix: torch.Tensor,
+    config: MPCConfig,
+    return_full: bool = False,
+    with_iters: bool = False,
+):
+    """Batched mean-variance solve on the device (kmpc_solve_mv).
+
+    Args:
+        current_weights: [B, N] device tensor (float64; other dtypes are converted).
+        mu: [B, H, N] expected returns (the reference passes predicted log-returns / the rolling
+            mean as mu, mpc.py:150-155); computed in float64.
+        cov_matrix: [B, N, N] per-window covariance, or one shared [N, N] (mpc.py:123).
+        config: MPCConfig (gamma, cost_coeff, allow_short; max_turnover is not part of this
+            program in the reference either).
+        return_full: return W [B, H, N] instead of W[:, 0].
+
+    Returns:
+        (W, status, value[, iters]) as solve_mpc_log_utility_batched; value is problem.value
+        (mpc.py:172, maximize form), NaN where the fallback was applied.
+    """
+    _lib.require_gpu(mu)
+    if mu.dim() != 3:
+        raise ValueError("mu must be [B, H, N]")
+    B, H, N = mu.shape
+    dev = mu.device
+    mu64 = mu.to(torch.float64).contiguous()
+    wp = current_weights.to(device=dev, dtype=torch.float64).contiguous()
+    if wp.shape != (B, N):
+        raise ValueError(f"current_weights must be [{B}, {N}], got {tuple(wp.shape)}")
+    S = torch.as_tensor(cov_matrix).to(device=dev, dtype=torch.float64).contiguous()
+    if S.dim() == 2:
+        if S.shape != (N, N):
+            raise ValueError(f"cov_matrix must be [{N}, {N}] or [{B}, {N}, {N}]")
+        stride = 0
+    elif S.shape == (B, N, N):
+        stride = N * N
+    else:
+        raise ValueError(f"cov_matrix must be [{N}, {N}] or [{B}, {N}, {N}], got {tuple(S.shape)}")
+    if H > _lib.KMPC_MV_MAX_H or H * N > _lib.KMPC_MV_MAX_HN:
+        raise _lib.KmpcError(f"mean-variance shape H={H}, N={N} exceeds the kernel limits "
+                             f"(H <= {_lib.KMPC_MV_MAX_H}, H*N <= {_lib.KMPC_MV_MAX_HN})")
+    W = torch.empty((B, H, N) if return_full else (B, N), dtype=torch.float64, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    value = torch.empty(B, dtype=torch.float64, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    d = _lib.MvDesc()
+    d.B, d.N, d.H = int(B), int(N), int(H)
+    d.gamma = float(config.gamma)
+    d.cost_coeff = float(config.cost_coeff)
+    d.allow_short = int(bool(config.allow_short))
+    d.max_iter = int(getattr(config, "mv_max_iter", 100))
+    d.tol = float(getattr(config, "mv_tol", 1e-10))
+    d.return_full_W = int(bool(return_full))
+    L = _lib.load()
+    with torch.cuda.device(dev):
+        rc = L.kmpc_solve_mv(ctypes.byref(d), mu64.data_ptr(), S.data_ptr(), stride, wp.data_ptr(),
+                             W.data_ptr(), status.data_ptr(), value.data_ptr(), iters.data_ptr(),
+                             _lib.stream_handle(dev))
+    _lib.check(rc)
+    if with_iters:
+        return W, status, value, iters
+    return W, status, value
+
+
+def solve_mpc_mean_variance(
+    current_weights: np.ndarray,
+    predicted_log_returns: np.ndarray,
+    cov_matrix: np.ndarray,
+    config: MPCConfig,
+) -> Tuple[np.ndarray, Dict]:
+    """Drop-in for mpc.py:119-184: returns (W [H, N] float64, info). On a non-optimal status the
+    reference returns tile(current_weights) and {"status": s} without a "value" key (mpc.py:180-181)."""
+    y = np.asarray(predicted_log_returns)
+    H, N = y.shape
+    dev = _default_device()
+    mu = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float64), device=dev).reshape(1, H, N)
+    wt = torch.as_tensor(np.asarray(current_weights, dtype=np.float64), device=dev).reshape(1, N)
+    S = torch.as_tensor(np.asarray(cov_matrix, dtype=np.float64), device=dev)
+    W, status, value = solve_mpc_mean_variance_batched(wt, mu, S, config, return_full=True)
+    st = _lib.STATUS_NAMES.get(int(status.item()), "solver_error")
+    if st not in ("optimal", "optimal_inaccurate"):
+        return np.tile(np.asarray(current_weights, dtype=np.float64), (H, 1)), {"status": st}
+    return W[0].cpu().numpy(), {"status": st, "value": float(value.item())}

@@ -48,6 +48,15 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_backtest_metrics(None, None, None, None) == -1
     bt.P = 0
     assert lib.kmpc_backtest_metrics(ctypes.byref(bt), None, None, None) == 0
+    mv = _lib.MvDesc()
+    mv.B, mv.N, mv.H = 1, 20, 0
+    assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == -1
+    mv.H, mv.N = 1, 129                                       # H * N > KMPC_MV_MAX_HN
+    assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == -2
+    mv.N, mv.B = 20, 0
+    assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == 0
+    assert lib.kmpc_rolling_moments(1, 10, 3, 0, None, 3, None, None, None, None, None, None, None) == -1
+    assert lib.kmpc_rolling_moments(0, 10, 3, 60, None, 3, None, None, None, None, None, None, None) == 0
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -64,18 +73,21 @@ int main(void) {{
          offsetof(kmpc_rollout_desc, std));
   printf("%zu\\n", offsetof(kmpc_rollout_desc, obs_ld));
   printf("%zu %zu\\n", sizeof(kmpc_backtest_desc), offsetof(kmpc_backtest_desc, cost_coeff));
+  printf("%zu %zu %zu %zu\\n", sizeof(kmpc_mv_desc), offsetof(kmpc_mv_desc, gamma),
+         offsetof(kmpc_mv_desc, tol), offsetof(kmpc_mv_desc, return_full_W));
   return 0;
 }}
 ''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", str(prog), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    S, M, R, Bt = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc, _lib.BacktestDesc
+    S, M, R, Bt, Mv = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc, _lib.BacktestDesc, _lib.MvDesc
     expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
               ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
               R.obs_ld.offset,
-              ctypes.sizeof(Bt), Bt.cost_coeff.offset]
+              ctypes.sizeof(Bt), Bt.cost_coeff.offset,
+              ctypes.sizeof(Mv), Mv.gamma.offset, Mv.tol.offset, Mv.return_full_W.offset]
     assert [int(x) for x in out] == expect
 
 
@@ -95,6 +107,13 @@ def test_reference_api_surface():
         ["self", "model", "mpc_config", "device"]
     assert list(inspect.signature(pkg.KoopmanMPCStrategy.rebalance).parameters) == \
         ["self", "t", "current_weights", "env", "lookback_window"]
+    assert list(inspect.signature(pkg.solve_mpc_mean_variance).parameters) == \
+        ["current_weights", "predicted_log_returns", "cov_matrix", "config"]
+    from koopman_mpc_portfolio_rebalancing_amd.baselines import MarkowitzStrategy
+    m = MarkowitzStrategy(risk_aversion=2.0, cost_coeff=0.01)     # reference tests/test_baselines.py:22-27
+    assert (m.risk_aversion, m.cost_coeff, m.mpc_config.gamma, m.mpc_config.horizon) == (2.0, 0.01, 2.0, 1)
+    assert list(inspect.signature(MarkowitzStrategy.__init__).parameters) == \
+        ["self", "risk_aversion", "cost_coeff", "allow_short"]
 
 
 def test_product_path_fails_loudly_without_gpu():
@@ -106,6 +125,11 @@ def test_product_path_fails_loudly_without_gpu():
     with pytest.raises(_lib.KmpcError):
         pkg.solve_mpc_log_utility_batched(torch.ones(1, 2, dtype=torch.float64) / 2, torch.zeros(1, 1, 2),
                                           pkg.MPCConfig(horizon=1))
+    with pytest.raises(_lib.KmpcError):
+        pkg.solve_mpc_mean_variance(np.array([0.5, 0.5]), np.zeros((1, 2)), np.eye(2), pkg.MPCConfig(horizon=1))
+    from koopman_mpc_portfolio_rebalancing_amd.baselines import MarkowitzStrategy
+    with pytest.raises(_lib.KmpcError):
+        MarkowitzStrategy().rebalance(10, np.array([0.5, 0.5]), None)
 
 
 def test_compat_shims_expose_reference_module_names():
