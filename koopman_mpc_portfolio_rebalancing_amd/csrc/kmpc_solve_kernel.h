@@ -66,6 +66,8 @@ struct PhaseClock {};
 #endif
 // refinement stops at ||r||_inf <= REFINE_RTOL ||b||_inf (the oracle uses the same rule)
 constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
+// corrector refinement only once the complementarity is this small (the oracle uses the same rule)
+constexpr double REFINE_MU = 1e-6;
 
 __host__ __device__ constexpr int pow2_at_least(int x) {
     int p = 1;
@@ -283,7 +285,7 @@ struct Shared {
     double bs[KM];              // Schur right-hand side, then solution q
     double red[2][NWM][RW];     // double-buffered reduction slots
     // per-period scalars
-    double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], l4[HM], nu[HM];
+    double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM];
     double rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     double t_adw[HM], t_sds[HM], t_sdw[HM];
@@ -295,11 +297,11 @@ struct Thread {
     static constexpr bool L = cold_in_lds<HM, MAXT>();
     int H, N, i;
     bool act, hw, hs, ht;
-    double c, tau, sig, irsig, wpi;
+    double c, tau, sig, isig, irsig, wpi;
     // state
     double w[HM], s[HM], l1[HM], l2[HM], l3[HM], m[HM];
     // per iteration: LDL^T of Q, P = 1/(alpha+beta); slack reciprocals (cold)
-    double P[HM], Dd[HM], Lr[HM];
+    double P[HM], iDd[HM], Lr[HM];
     Cold<HM, MAXT, L> iw, iz2, iz3;
     // complementarity targets rc = z*l (- sigma mu + dz_aff dl_aff) (cold)
     Cold<HM, MAXT, L> rc1, rc2, rc3;
@@ -313,7 +315,8 @@ struct Thread {
     __device__ __forceinline__ double wprev(int t) const { return t ? w[t - 1] : wpi; }
     __device__ __forceinline__ double bma(int t) const { return l3[t] * iz3[t] - l2[t] * iz2[t]; }
 
-    // x = Q^{-1} r  (LDL^T: y_t = r_t + Lr_t y_{t-1};  x_t = y_t / Dd_t + Lr_{t+1} x_{t+1})
+    // x = Q^{-1} r  (LDL^T: y_t = r_t + Lr_t y_{t-1};  x_t = y_t / Dd_t + Lr_{t+1} x_{t+1}),
+    // with the pivots kept as reciprocals iDd = 1 / Dd (no divisions in the solves)
     __device__ __forceinline__ void qsolve(const double (&r)[HM], double (&x)[HM]) const {   // may alias
         double y = 0.0;
 #pragma unroll
@@ -321,7 +324,7 @@ struct Thread {
         double nxt = 0.0;
 #pragma unroll
         for (int t = HM - 1; t >= 0; --t) {
-            const double v = x[t] / Dd[t] + ((t + 1 < HM) ? Lr[t + 1] * nxt : 0.0);
+            const double v = x[t] * iDd[t] + ((t + 1 < HM) ? Lr[t + 1] * nxt : 0.0);
             x[t] = (t < H) ? v : 0.0;
             nxt = x[t];
         }
@@ -461,7 +464,7 @@ __device__ __forceinline__ void dual_residual(const Thread<HM, NWM * WAVE>& T, c
                                               double& rdw, double& rds) {
     const double eta = T.l3[t] - T.l2[t];
     const double etan = (t + 1 < HM && t + 1 < T.H) ? T.l3[t + 1] - T.l2[t + 1] : 0.0;
-    rdw = -T.m[t] * sh.iden[t] / T.sig - (T.l1[t] + eta - etan) + sh.nu[t];
+    rdw = -T.m[t] * sh.iden[t] * T.isig - (T.l1[t] + eta - etan) + sh.nu[t];
     rds = T.hs ? T.c - (T.l2[t] + T.l3[t] - sh.l4[t]) : 0.0;
 }
 
@@ -486,7 +489,7 @@ __device__ __forceinline__ void lsolve(const Thread<HM, NWM * WAVE>& T, Shared<H
         }
         const bool on = T.act && t < H;
         bw[t] = on ? bw[t] + p1 + (p3 - p2) - pn : 0.0;                                   // rhs_w
-        bs[t] = (on && T.hs) ? bs[t] + p2 + p3 - (T.ht ? sh.lb5[t] / sh.z4[t] : 0.0) : 0.0;  // rhs_s
+        bs[t] = (on && T.hs) ? bs[t] + p2 + p3 - (T.ht ? sh.lb5[t] * sh.iz4[t] : 0.0) : 0.0;  // rhs_s
     }
     // (diag(alpha+beta) + gamma 1 1')^{-1} x per period = P (x - rho 1'P x)
     double px[HM], tq[HM];
@@ -675,7 +678,7 @@ __device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
                 double rdw, rds;
                 dual_residual<HM, NWM>(T, sh, t, rdw, rds);
                 const double al = T.m[t] * sh.iden[t] * T.irsig;
-                const double dl4 = T.ht ? (sh.b5[t] + sh.l4[t] * sds[t]) / sh.z4[t] : 0.0;
+                const double dl4 = T.ht ? (sh.b5[t] + sh.l4[t] * sds[t]) * sh.iz4[t] : 0.0;
                 r0[t] = -rdw - (al * adw[t] - (dl1 + (dl3 - dl2) - (nl3 - nl2)) + sh.dnu[t]);
                 r1[t] = T.hs ? -rds + (dl2 + dl3 - dl4) : 0.0;
             } else {
@@ -711,7 +714,7 @@ __device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
         for (int k = 0; k < HM; ++k) if (k == t) st = sds[k];
         const bool on = T.ht && t < H;
         sh.dz4[t] = on ? -st + sh.rg4[t] : 0.0;
-        sh.dl4[t] = on ? (sh.b5[t] + sh.l4[t] * st) / sh.z4[t] : 0.0;
+        sh.dl4[t] = on ? (sh.b5[t] + sh.l4[t] * st) * sh.iz4[t] : 0.0;
     }
     __syncthreads();
     KMPC_PH(np, 15);
@@ -828,15 +831,16 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
         double pi = W1[0] + E[0];
 #pragma unroll
         for (int t = 0; t < HM; ++t) {
-            T.Dd[t] = 1.0;
+            T.iDd[t] = 1.0;
             T.Lr[t] = 0.0;
             if (T.act && t < H) {
                 if (t > 0) {
-                    T.Lr[t] = E[t] / T.Dd[t - 1];
+                    T.Lr[t] = E[t] * T.iDd[t - 1];
                     pi = W1[t] + T.Lr[t] * pi;
                 }
-                T.Dd[t] = pi + ((t + 1 < HM && t + 1 < H) ? E[t + 1] : 0.0);
-                ok = ok && (T.Dd[t] > 0.0) && (T.Dd[t] < 1e300);
+                const double dd = pi + ((t + 1 < HM && t + 1 < H) ? E[t + 1] : 0.0);
+                ok = ok && (dd > 0.0) && (dd < 1e300);
+                T.iDd[t] = 1.0 / dd;
             }
         }
     }
@@ -846,7 +850,7 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
     for (int k = HM - 1; k >= 0; --k) {
         double v = 0.0;
         if (T.act && k < H) {
-            v = 1.0 / T.Dd[k];
+            v = T.iDd[k];
             if (k + 1 < HM) v += T.Lr[k + 1] * T.Lr[k + 1] * dq[k + 1];
         }
         dq[k] = v;
@@ -1127,6 +1131,7 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
     double sig = fmax(mx, args.c);
     if (!(sig > 0.0)) sig = 1.0;
     T.sig = sig;
+    T.isig = 1.0 / sig;
     T.irsig = 1.0 / sqrt(sig);
     T.c = args.c / sig;
 
@@ -1214,6 +1219,7 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                         sh.rp[t] = on ? b2 - 1.0 : 0.0;
                         sh.rg4[t] = (T.ht && on) ? T.tau - c2 - sh.z4[t] : 0.0;
                         sh.rc4[t] = (T.ht && on) ? sh.z4[t] * sh.l4[t] : 0.0;
+                        sh.iz4[t] = 1.0 / sh.z4[t];
                     }
                     __syncthreads();
                 }
@@ -1272,8 +1278,9 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 double step = 0.0;
                 for (int pass = 0; pass < 2; ++pass) {
                     // predictor unrefined (it only sets the step estimate, sigma and the
-                    // second-order term), corrector refined adaptively — as the oracle
-                    newton<HM, NWM>(T, sh, R, pass == 0 ? 0 : args.n_refine);
+                    // second-order term); corrector refined adaptively once mu <= REFINE_MU
+                    // (before that G is well conditioned and the IPM self-corrects) — as the oracle
+                    newton<HM, NWM>(T, sh, R, (pass == 0 || mu > REFINE_MU) ? 0 : args.n_refine);
                     KMPC_PH(ph, 4);
                     const double amax = max_step<HM, NWM>(T, sh, R);
                     if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }

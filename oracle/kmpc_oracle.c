@@ -603,7 +603,12 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
                 }
                 if (W.ht) W.rc4[t] += W.dz4[t] * W.dl4[t] - sg * mu;
             }
-            newton(&W);
+            {   /* corrector refinement only once mu <= 1e-6 (the kernel's REFINE_MU) */
+                const int nr = W.n_refine;
+                if (mu > R_(1e-6)) W.n_refine = 0;
+                newton(&W);
+                W.n_refine = nr;
+            }
             /* one step length for primal and dual: the objective is nonlinear, so unequal steps
                would re-inject dual residual (alpha_p - alpha_d) Hf dw */
             real a = RFMIN(1, R_(0.99) * max_step(&W));

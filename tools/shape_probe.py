@@ -1,0 +1,24 @@
+"""Dev probe: solve-kernel throughput at the BASELINE config shapes (not the benchmark).
+usage: python tools/shape_probe.py [B_C5]"""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from koopman_mpc_portfolio_rebalancing_amd import MPCConfig, solve_mpc_log_utility_batched
+
+def run(name, B, N, H, cost, tau, reps=2):
+    rng = np.random.default_rng(0)
+    wp = torch.tensor(rng.dirichlet(np.ones(N), B), device="cuda")
+    y = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device="cuda")
+    cfg = MPCConfig(horizon=H, cost_coeff=cost, max_turnover=tau)
+    solve_mpc_log_utility_batched(wp[:64], y[:64], cfg); torch.cuda.synchronize()
+    for _ in range(reps):
+        t = time.time()
+        W, st, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
+        torch.cuda.synchronize(); dt = time.time() - t
+    print(f"{name}: B={B} N={N} H={H} {dt*1e3:.1f} ms {B/dt:.0f} windows/s iters {it.float().mean().item():.1f} "
+          f"status {np.bincount(st.cpu().numpy(), minlength=5)}", flush=True)
+
+run("C2", 4096, 30, 5, 0.0, 0.0)
+run("C1-shape", 4096, 10, 5, 1e-3, 0.2)
+run("C3", 16384, 100, 10, 1e-3, 0.2)
+run("C5", int(sys.argv[1]) if len(sys.argv) > 1 else 1024, 500, 20, 1e-3, 0.2, reps=1)
