@@ -39,6 +39,9 @@ sys.path.insert(0, ROOT)
 METRIC = "MPC window-solves/sec (batched backtest) at 1/2/4/8 MI355X vs host-CPU ref"
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
+# per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
+PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_solve_pmc.json")
 
 
 def parse():
@@ -171,12 +174,12 @@ def main():
         y = model.rollout(x, mean_d, std_d, H, N)
         if e is not None:
             e[1].record()
-        W0, st, val = solve_mpc_log_utility_batched(wp, y, cfg)
+        W0, st, val, its = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
         if e is not None:
             e[2].record()
         if world > 1:
             gather_rows(W0, world * B, world, rank, dst=0)
-        return y, W0, st, val
+        return y, W0, st, val, its
 
     for _ in range(args.warmup):
         step()
@@ -186,7 +189,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        y, W0, st, val = step(ev[k])
+        y, W0, st, val, its = step(ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -208,6 +211,18 @@ def main():
         # write W0 f64 [B,N] + status i32 + value f64 (+ iters i32) per window
         solve_bytes = B * (4 * H * N + 8 * N + 8 * N + 4 + 8 + 4)
         achieved = solve_bytes / (solve_ms * 1e-3)
+        # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scaled
+        # to this launch's windows) and the executed f64 VALU rate of the solve against its peak:
+        # the solver is bound by f64 latency / VALU, not by HBM
+        traffic, compute = None, None
+        if os.path.exists(PMC_JSON) and (N, H) == (100, 10):
+            pmc = json.load(open(PMC_JSON))
+            traffic = (pmc["fetch_bytes_per_window"] + pmc["write_bytes_per_window"]) * B
+            if "f64_flops_per_window" in pmc:
+                f64 = pmc["f64_flops_per_window"] * B / (solve_ms * 1e-3)
+                compute = {"bound": "valu_f64", "achieved": f64 / 1e12, "peak": F64_VALU_PEAK / 1e12,
+                           "unit": "TFLOP/s", "frac": f64 / F64_VALU_PEAK,
+                           "flops": "executed f64 VALU FLOPs per window from PMC (profiles/r01_solve_pmc.json)"}
         roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
                                 + H * (L * L + L * N))
         line = {
@@ -220,13 +235,15 @@ def main():
                        "windows_per_gpu": B, "global_windows_per_step": world * B,
                        "parallelism": f"windows sharded over {world} GPU(s), RCCL gather of W0"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": None,
-                         "kernel": "kmpc_solve (solve_kernel)",
+                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "kernel": "kmpc_solve (ipm_kernel<10,128,true>)",
                          "algorithmic_bytes_per_window": solve_bytes // B, "launch_ms": solve_ms},
+            "compute_roofline": compute,
             "kernels": {"rollout_ms": roll_ms, "solve_ms": solve_ms,
                         "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
                         "rollout_mfma_frac": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK},
-            "solver": {"optimal_or_inaccurate": n_opt, "windows": B},
+            "solver": {"optimal_or_inaccurate": n_opt, "windows": B,
+                       "mean_ipm_iterations": float(its.float().mean().item())},
         }
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
