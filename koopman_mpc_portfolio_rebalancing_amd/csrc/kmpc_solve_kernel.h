@@ -357,13 +357,24 @@ struct Reducer {
         constexpr int RW = Shared<HM, NWM>::RW;
         if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
         __syncthreads();
+        // the slot reads (uniform-address broadcasts) in flight together, in groups of <= 16
+        // doubles per lane, then the sums
+        constexpr int G = (16 / NWM) < M ? (16 / NWM > 0 ? 16 / NWM : 1) : M;
 #pragma unroll
-        for (int j = 0; j < M; ++j) {
-            double s = r[j];
+        for (int j0 = 0; j0 < M; j0 += G) {
+            double t[NWM][G];
 #pragma unroll
-            for (int q = 1; q < NWM; ++q)
-                if (q < nw) s += r[q * RW + j];
-            v[j] = s;
+            for (int q = 0; q < NWM; ++q)
+#pragma unroll
+                for (int j = 0; j < G; ++j) t[q][j] = (q == 0 || q < nw) ? r[q * RW + j0 + j] : 0.0;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                double s = t[0][j];
+#pragma unroll
+                for (int q = 1; q < NWM; ++q) s += t[q][j];
+                v[j0 + j] = s;
+            }
         }
         buf ^= 1;
     }
@@ -1035,7 +1046,11 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
         for (int j = 0; j < KM; ++j) {
             const double d = bcast(g[j], j);
             bad = bad || !(d > 0.0) || !(d < 1e300);
-            const double id = 1.0 / fmax(d, 1e-300);
+            // 1 / d: v_rcp_f64 + two Newton steps (~1 ulp; the chain is latency bound)
+            const double dm = fmax(d, 1e-300);
+            double id = __builtin_amdgcn_rcp(dm);
+            id = fma(id, fma(-dm, id, 1.0), id);
+            id = fma(id, fma(-dm, id, 1.0), id);
             const double u = g[j];                    // row r of the updated column j
             const double l = (r > j) ? u * id : 0.0;  // L_rj
             if (r == j) dinv = id;
@@ -1043,8 +1058,13 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
             if (j + 1 < KM) {
                 sh.col[r] = u;
                 __builtin_amdgcn_wave_barrier();
+                // all reads of the column in flight at once (one LDS round trip per step)
+                double cv[KM];
 #pragma unroll
-                for (int k = j + 1; k < KM; ++k) g[k] = fma(-l, sh.col[k], g[k]);
+                for (int k = j + 1; k < KM; ++k) cv[k] = sh.col[k];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = j + 1; k < KM; ++k) g[k] = fma(-l, cv[k], g[k]);
                 __builtin_amdgcn_wave_barrier();
             }
         }
