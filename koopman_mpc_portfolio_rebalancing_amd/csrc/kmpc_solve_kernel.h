@@ -330,6 +330,35 @@ struct Thread {
         }
     }
 
+    // multipliers of the current direction for every period at once: the cold LDS reads of a
+    // group of periods are issued together (one round trip per group) and nothing branches, so
+    // the callers' per-period bodies wait on no LDS read. Inactive lanes / periods have zero
+    // targets and reciprocals (factor(), the rc loop) and get zero multipliers.
+    __device__ __forceinline__ void dual_dirs_all(double (&dl1)[HM], double (&dl2)[HM], double (&dl3)[HM]) const {
+        constexpr int G = 5;
+#pragma unroll
+        for (int t0 = 0; t0 < HM; t0 += G) {
+            double c[6][G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int t = t0 + j < HM ? t0 + j : HM - 1;
+                c[0][j] = rc1[t]; c[1][j] = rc2[t]; c[2][j] = rc3[t];
+                c[3][j] = iw[t]; c[4][j] = iz2[t]; c[5][j] = iz3[t];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int t = t0 + j;
+                if (t < HM) {
+                    const double dd = dw[t] - (t ? dw[t - 1] : 0.0);
+                    dl1[t] = hw ? (-c[0][j] - l1[t] * dw[t]) * c[3][j] : 0.0;
+                    dl2[t] = hs ? (-c[1][j] - l2[t] * (ds[t] - dd)) * c[4][j] : 0.0;
+                    dl3[t] = hs ? (-c[2][j] - l3[t] * (ds[t] + dd)) * c[5][j] : 0.0;
+                }
+            }
+        }
+    }
+
     // multipliers of the current direction (complementarity rows with targets rc)
     __device__ __forceinline__ void dual_dirs(int t, double& dl1, double& dl2, double& dl3) const {
         const double dd = dw[t] - (t ? dw[t - 1] : 0.0);
@@ -736,12 +765,13 @@ template <int HM, int NWM>
 __device__ __forceinline__ double max_step(const Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R) {
     const int H = T.H;
     double a = 1e300, mdw[HM];
+    double DL1[HM], DL2[HM], DL3[HM];
+    T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         mdw[t] = 0.0;
         if (T.act && t < H) {
-            double dl1, dl2, dl3;
-            T.dual_dirs(t, dl1, dl2, dl3);
+            const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
             const double d = T.w[t] - T.wprev(t);
             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
             if (T.hw) { a = to_bound(T.w[t], T.dw[t], a); a = to_bound(T.l1[t], dl1, a); }
@@ -771,11 +801,12 @@ __device__ __forceinline__ double complementarity(const Thread<HM, NWM * WAVE>& 
                                                   Reducer<HM, NWM>& R, double a) {
     const int H = T.H;
     double acc = 0.0;
+    double DL1[HM], DL2[HM], DL3[HM];
+    T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         if (T.act && t < H) {
-            double dl1, dl2, dl3;
-            T.dual_dirs(t, dl1, dl2, dl3);
+            const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
             const double d = T.w[t] - T.wprev(t);
             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
             if (T.hw) acc += (T.w[t] + a * T.dw[t]) * (T.l1[t] + a * dl1);
@@ -1308,11 +1339,12 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                     double sg = complementarity<HM, NWM>(T, sh, R, ap) * inv_ncon / mu;
                     sg = sg * sg * sg;
                     const double smu = sg * mu;
+                    double DL1[HM], DL2[HM], DL3[HM];
+                    T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
                         if (T.act && t < H) {
-                            double dl1, dl2, dl3;
-                            T.dual_dirs(t, dl1, dl2, dl3);
+                            const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
                             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
                             if (T.hw) T.rc1.set(t, T.rc1[t] + (T.dw[t] * dl1 - smu));
                             if (T.hs) {
@@ -1330,14 +1362,16 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 if (args.trace && b == 0 && threadIdx.x == 0) args.trace[4 * it + 3] = step;
                 KMPC_PH(ph, 5);
                 // ---- update ----
+                {
+                    double DL1[HM], DL2[HM], DL3[HM];
+                    T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    if (T.act && t < H) {
-                        double dl1, dl2, dl3;
-                        T.dual_dirs(t, dl1, dl2, dl3);
-                        T.l1[t] += step * dl1;
-                        T.l2[t] += step * dl2;
-                        T.l3[t] += step * dl3;
+                    for (int t = 0; t < HM; ++t) {
+                        if (T.act && t < H) {
+                            T.l1[t] += step * DL1[t];
+                            T.l2[t] += step * DL2[t];
+                            T.l3[t] += step * DL3[t];
+                        }
                     }
                 }
 #pragma unroll

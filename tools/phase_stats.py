@@ -7,7 +7,17 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 N, H = 100, 10
 rng = np.random.default_rng(0)
 wp = torch.tensor(rng.dirichlet(np.ones(N), B), device="cuda")
-y = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device="cuda")
+if os.environ.get("BENCH_Y", "1") == "1":
+    # the benchmark's own yhat: bench.py's seeded finance_sparse model rolled out on its inputs
+    import bench
+    from koopman_mpc_portfolio_rebalancing_amd import DeviceKoopman, KoopmanModelSpec
+    sd = bench.make_state_dict(N * 20, 256, 1024, seed=0)
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), torch.device("cuda", 0))
+    torch.manual_seed(1000)
+    x, _ = bench.make_inputs(B, N, N * 20, seed=0, device=torch.device("cuda", 0))
+    y = km.rollout(x, np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32), H, N)
+else:
+    y = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device="cuda")
 from oracle import solver as oracle
 nchk = 64
 Wo, sto, vo, _ = oracle.solve_batch(wp[:nchk].cpu().numpy(), y[:nchk].cpu().numpy(), 1e-3, 0.2, precision="ld")
