@@ -94,6 +94,8 @@ int kmpc_solve(const kmpc_solve_desc* desc,
 #define KMPC_NORM_ID   0
 #define KMPC_NORM_BALL 1
 #define KMPC_MAX_LAYERS 8
+#define KMPC_DTYPE_F32  0
+#define KMPC_DTYPE_BF16 1
 
 /*
  * An MLP (model.py:67-117, MLPCoder): n_layers Linear layers with dims[0] -> dims[1] -> ... ->
@@ -137,6 +139,9 @@ typedef struct kmpc_rollout_desc {
                                  rows i .. i+d-1 (kmpc_standardize below) — the time-delay
                                  embedding without materialising it; the first encoder layer's
                                  column blocks must then be in oldest-lag-first order.          */
+    int dtype;                /* KMPC_DTYPE_F32 (0, the reference's arithmetic) or KMPC_DTYPE_BF16 (1:
+                                 GEMM operands rounded to bf16 on MFMA, fp32 accumulation and
+                                 epilogues; BASELINE configs[4])                                 */
 } kmpc_rollout_desc;
 
 int kmpc_rollout(const kmpc_rollout_desc* desc,

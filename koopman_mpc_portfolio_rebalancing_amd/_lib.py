@@ -22,6 +22,7 @@ KMPC_MAX_H = 21          # the Schur system (3H rows) is factored by one 64-lane
 MODEL_GENERIC, MODEL_LISTA = 0, 1
 ACT = {"relu": 0, "tanh": 1, "gelu": 2}
 NORM = {"id": 0, "ball": 1}
+DTYPE = {"fp32": 0, "bf16": 1}
 
 STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
                 4: "solver_error"}
@@ -64,7 +65,8 @@ class RolloutDesc(ctypes.Structure):
                 ("obs", ctypes.c_int), ("model_kind", ctypes.c_int), ("norm_fn", ctypes.c_int),
                 ("encoder", Mlp), ("lista_S", ctypes.c_void_p), ("lista_loops", ctypes.c_int),
                 ("lista_thresh", ctypes.c_float), ("kmat", ctypes.c_void_p), ("decoder", Mlp),
-                ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p), ("obs_ld", ctypes.c_int)]
+                ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p), ("obs_ld", ctypes.c_int),
+                ("dtype", ctypes.c_int)]
 
 
 class BacktestDesc(ctypes.Structure):

@@ -8,7 +8,9 @@
 //                                          data_finance.py:729 (slice), :740-742 (de-standardize)
 //
 // Every dense contraction is one fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32: exact fp32 products,
-// fp32 accumulation, the arithmetic type of the reference's torch fp32 path) with a fused epilogue
+// fp32 accumulation, the arithmetic type of the reference's torch fp32 path) — or, with
+// desc->dtype = KMPC_DTYPE_BF16, a bf16 MFMA GEMM (operands rounded to bf16, fp32 accumulation;
+// BASELINE configs[4]) — with a fused epilogue
 // (bias + activation, LISTA shrink, de-standardize-and-scatter). Only the first N decoder rows are
 // evaluated. Weights in the reference's nn.Linear [out, in] layout are consumed as-is ("NT");
 // K and S (right-multiplied, [in, out]) are transposed once per call into the workspace.
@@ -22,6 +24,8 @@ namespace kmpc {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 enum Epi : int {
     EPI_NONE = 0,        // out = acc (+ bias)
@@ -40,6 +44,7 @@ struct GemmArgs {
     const float* R; int ldr;      // EPI_SHRINK addend [M, N]
     float thr;
     const float* mean; const float* stdv;   // EPI_DESTD [N]
+    int bf16;                     // 1: operands rounded to bf16, v_mfma_f32_32x32x16_bf16 (fp32 accumulate)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -61,6 +66,39 @@ __device__ __forceinline__ float destandardize(float y, float sd, float mu) {
 #pragma clang fp contract(off)
     const float p = y * sd;
     return p + mu;
+}
+
+// fused epilogue of a 2 x 2 block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D layout
+// is dtype-independent on gfx950)
+__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0, int wm, int wn,
+                                         int lane) {
+    // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int n = n0 + wn + b * 32 + (lane & 31);
+            if (n >= g.N) continue;
+            const float bias = g.bias ? g.bias[n] : 0.0f;
+            float mu = 0.0f, sd = 1.0f;
+            if (g.epi == EPI_DESTD) { mu = g.mean[n]; sd = g.stdv[n]; }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m >= g.M) continue;
+                float v = acc[a][b][r] + bias;
+                if (g.epi == EPI_ACT) {
+                    v = apply_act(v, g.act);
+                } else if (g.epi == EPI_SHRINK) {
+                    v += g.R[(size_t)m * g.ldr + n];
+                    const float av = fabsf(v) - g.thr;
+                    v = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
+                } else if (g.epi == EPI_DESTD) {
+                    v = destandardize(v, sd, mu);
+                }
+                g.C[(size_t)m * g.ldc + n] = v;
+            }
+        }
 }
 
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
@@ -127,33 +165,76 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         __syncthreads();
     }
-    // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+    epilogue(g, acc, m0, n0, wm, wn, lane);
+}
+
+// bf16 variant (BASELINE configs[4]: "bf16 MFMA rollout"): the same 128 x 128 tile and epilogues;
+// A and B are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) while being staged into LDS, the products
+// run on v_mfma_f32_32x32x16_bf16 with fp32 accumulation. Lane (r, h) of a 32x32x16 step holds
+// A[row r][k = 8h + j] and B[col r][k = 8h + j], j = 0..7: one ds_read_b128 per operand per step.
+constexpr int LDS_STRIDE_H = BK + 8;   // bf16 elements per LDS row (80 B: 16-B aligned fragments)
+
+__global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
+    __shared__ __bf16 As[BM * LDS_STRIDE_H];
+    __shared__ __bf16 Bs[BN * LDS_STRIDE_H];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+    f32x16 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int n = n0 + wn + b * 32 + (lane & 31);
-            if (n >= g.N) continue;
-            const float bias = g.bias ? g.bias[n] : 0.0f;
-            float mu = 0.0f, sd = 1.0f;
-            if (g.epi == EPI_DESTD) { mu = g.mean[n]; sd = g.stdv[n]; }
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (m >= g.M) continue;
-                float v = acc[a][b][r] + bias;
-                if (g.epi == EPI_ACT) {
-                    v = apply_act(v, g.act);
-                } else if (g.epi == EPI_SHRINK) {
-                    v += g.R[(size_t)m * g.ldr + n];
-                    const float av = fabsf(v) - g.thr;
-                    v = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
-                } else if (g.epi == EPI_DESTD) {
-                    v = destandardize(v, sd, mu);
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+    const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
+                        ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int idx = tid + q * 256;          // 0..1023: 128 rows x 8 groups of 4 k
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int kk = k0 + c4;
+            f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+            const int ma = m0 + row, nb = n0 + row;
+            if (vec_ok && kk + 3 < g.K) {
+                if (ma < g.M) va = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
+                if (nb < g.N) vb = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (kk + e < g.K) {
+                        if (ma < g.M) va[e] = g.A[(size_t)ma * g.lda + kk + e];
+                        if (nb < g.N) vb[e] = g.B[(size_t)nb * g.ldb + kk + e];
+                    }
                 }
-                g.C[(size_t)m * g.ldc + n] = v;
             }
+            bf16x4 ha, hb;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { ha[e] = (__bf16)va[e]; hb[e] = (__bf16)vb[e]; }
+            *(bf16x4*)(As + row * LDS_STRIDE_H + c4) = ha;
+            *(bf16x4*)(Bs + row * LDS_STRIDE_H + c4) = hb;
         }
+        __syncthreads();
+        const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+        for (int st = 0; st < BK / 16; ++st) {
+            bf16x8 af[2], bfr[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                af[a] = *(const bf16x8*)(As + (wm + a * 32 + r) * LDS_STRIDE_H + 16 * st + 8 * h);
+                bfr[a] = *(const bf16x8*)(Bs + (wn + a * 32 + r) * LDS_STRIDE_H + 16 * st + 8 * h);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    epilogue(g, acc, m0, n0, wm, wn, lane);
 }
 
 // shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
@@ -198,7 +279,8 @@ __global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
 static int gemm(const GemmArgs& g, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    hipLaunchKernelGGL(gemm_nt_kernel, grid, dim3(256), 0, s, g);
+    if (g.bf16) hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL(gemm_nt_kernel, grid, dim3(256), 0, s, g);
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 
@@ -237,7 +319,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
 // layer, written with row stride ldo); ping/pong are [B, wmax] scratch buffers.
 static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* out, int ldo,
                    int last_cols, int last_epi, const float* mean, const float* stdv, float* ping,
-                   float* pong, int wmax, hipStream_t s) {
+                   float* pong, int wmax, int bf16, hipStream_t s) {
     const float* cur = X;
     int ldc = ldx;
     for (int l = 0; l < m.n_layers; ++l) {
@@ -246,6 +328,7 @@ static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* ou
         float* dst = last ? out : ((l & 1) ? pong : ping);
         GemmArgs g = linear(Bn, nout, m.dims[l], cur, ldc, m.weight[l], m.bias[l], dst,
                             last ? ldo : wmax);
+        g.bf16 = bf16;
         if (!last) { g.epi = EPI_ACT; g.act = m.act; }
         else if (last_epi == EPI_DESTD) { g.epi = EPI_DESTD; g.mean = mean; g.stdv = stdv; }
         else if (m.last_relu) { g.epi = EPI_ACT; g.act = KMPC_ACT_RELU; }
@@ -268,6 +351,8 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (d->model_kind == KMPC_MODEL_LISTA && !d->lista_S) return KMPC_ERR_INVALID;
     if (ws_bytes < rollout_workspace_bytes(d) || (!ws && ws_bytes)) return KMPC_ERR_WORKSPACE;
     if (d->obs_ld < 0 || (d->obs_ld > 0 && d->obs_ld < d->N)) return KMPC_ERR_INVALID;
+    if (d->dtype != KMPC_DTYPE_F32 && d->dtype != KMPC_DTYPE_BF16) return KMPC_ERR_INVALID;
+    const int bf = d->dtype == KMPC_DTYPE_BF16;
     if (d->B == 0) return KMPC_OK;
     const int Bn = d->B, L = d->L, N = d->N, H = d->H;
     const int obs_ld = d->obs_ld > 0 ? d->obs_ld : d->obs;
@@ -293,13 +378,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
 
     // ---- encode ----
     if (d->model_kind == KMPC_MODEL_GENERIC) {
-        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s);
         if (rc) return rc;
         if (d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, z0, Bn, L);
     } else {
         // c = We(x) (z1 holds c), z = shrink(c); loops: z = shrink(z S + c)   (model.py:200-209)
-        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s);
         if (rc) return rc;
         const size_t n = (size_t)Bn * L;
         hipLaunchKernelGGL(shrink_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z1, z0, n,
@@ -308,11 +393,12 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         float* zn = ping;   // ping is [B, wmax] >= [B, L]
         for (int it = 0; it < d->lista_loops; ++it) {
             GemmArgs g = linear(Bn, L, L, zc, L, St, nullptr, zn, L);
-            g.epi = EPI_SHRINK; g.R = z1; g.ldr = L; g.thr = d->lista_thresh;
+            g.epi = EPI_SHRINK; g.R = z1; g.ldr = L; g.thr = d->lista_thresh; g.bf16 = bf;
             if ((rc = gemm(g, s))) return rc;
             float* t = zc; zc = zn; zn = t;
         }
-        if (zc != z0) hipMemcpyAsync(z0, zc, sizeof(float) * n, hipMemcpyDeviceToDevice, s);
+        if (zc != z0 && hipMemcpyAsync(z0, zc, sizeof(float) * n, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return KMPC_ERR_LAUNCH;
     }
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
 
@@ -321,12 +407,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     float* zn = z1;
     for (int k = 0; k < H; ++k) {
         GemmArgs g = linear(Bn, L, L, zc, L, Kt, nullptr, zn, L);
+        g.bf16 = bf;
         if ((rc = gemm(g, s))) return rc;
         if (d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, zn, Bn, L);
         // decoder: hidden layers full width, last layer first-N rows + destandardize into yhat[:, k, :]
         rc = run_mlp(d->decoder, Bn, zn, L, yhat + (size_t)k * N, H * N, N, EPI_DESTD, d->mean, d->std,
-                     ping, pong, wmax, s);
+                     ping, pong, wmax, bf, s);
         if (rc) return rc;
         float* t = zc; zc = zn; zn = t;
     }

@@ -110,7 +110,12 @@ class KoopmanModelSpec:
 class DeviceKoopman:
     """A KoopmanModelSpec resident on one device, evaluated through kmpc_rollout / kmpc_window."""
 
-    def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None):
+    def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None, dtype: str = "fp32"):
+        """dtype: 'fp32' (the reference's arithmetic, default) or 'bf16' (GEMM operands rounded to
+        bf16 on the bf16 MFMA, fp32 accumulation — BASELINE configs[4])."""
+        if dtype not in _lib.DTYPE:
+            raise ValueError(f"dtype must be one of {sorted(_lib.DTYPE)}")
+        self.dtype = dtype
         if device is None:
             if not torch.cuda.is_available():
                 raise _lib.KmpcError("DeviceKoopman needs a GPU (libkmpc.so has no CPU path)")
@@ -160,6 +165,7 @@ class DeviceKoopman:
         d.norm_fn = _lib.NORM[s.norm_fn]
         d.encoder = self._mlp(enc if enc is not None else self.enc, s.enc_act, s.enc_last_relu)
         d.obs_ld = int(obs_ld)
+        d.dtype = _lib.DTYPE[self.dtype]
         d.lista_S = self.S.data_ptr() if self.S is not None else None
         d.lista_loops = int(s.lista_loops)
         d.lista_thresh = float(s.lista_thresh)

@@ -14,6 +14,9 @@ Follows, op for op, what ``KoopmanMPCStrategy.rebalance`` computes before the so
 
 Weights use the reference's state_dict layout (nn.Linear weight = [out, in]). The arithmetic is
 float32 like the reference's torch path; only the summation order of each dot product differs.
+With ``bf16=True`` every matrix-product operand is first rounded to bfloat16 (round to nearest
+even) and the products accumulate in float32 — the semantics of the device's bf16 MFMA rollout
+(kmpc_rollout with KMPC_DTYPE_BF16, BASELINE configs[4]); it is not a reference code path.
 """
 from __future__ import annotations
 
@@ -33,12 +36,27 @@ def _act(x, name):
     raise ValueError(name)
 
 
-def mlp(x, weights, biases, activation="relu", last_relu=False):
+def bf16_round(x):
+    """float32 -> nearest-even bfloat16, returned as float32 (v_cvt_pk_bf16_f32 semantics)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32).view(np.float32)
+
+
+def _mm(a, b, bf16=False):
+    """a @ b in float32, operands rounded to bf16 first when bf16."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    if bf16:
+        a, b = bf16_round(a), bf16_round(b)
+    return (a @ b).astype(np.float32)
+
+
+def mlp(x, weights, biases, activation="relu", last_relu=False, bf16=False):
     """MLPCoder.forward (model.py:67-117): Linear, act, ..., Linear (+ReLU if last_relu)."""
     h = np.asarray(x, np.float32)
     n = len(weights)
     for k, (W, b) in enumerate(zip(weights, biases)):
-        h = h @ np.asarray(W, np.float32).T
+        h = _mm(h, np.asarray(W, np.float32).T, bf16)
         if b is not None:
             h = h + np.asarray(b, np.float32)
         if k < n - 1:
@@ -69,8 +87,8 @@ def lista_decoder_weight(dict_param):
     return (d / nrm).T.astype(np.float32)                        # Linear weight layout [obs, L]
 
 
-def rollout(spec, obs, H, n_assets, mean, std):
-    """yhat [B, H, N] float32 for observations obs [B, obs].
+def rollout(spec, obs, H, n_assets, mean, std, bf16=False):
+    """yhat [B, H, N] float32 for observations obs [B, obs] (bf16: see the module docstring).
 
     spec: dict with
       kind: 'generic' | 'lista'
@@ -85,21 +103,22 @@ def rollout(spec, obs, H, n_assets, mean, std):
     K = np.asarray(spec["kmat"], np.float32)
     if spec["kind"] == "generic":
         z = norm_fn(mlp(x, spec["enc_w"], spec["enc_b"], spec.get("enc_act", "relu"),
-                        spec.get("enc_last_relu", False)), spec.get("norm_fn", "id"))
+                        spec.get("enc_last_relu", False), bf16), spec.get("norm_fn", "id"))
     else:
-        c = mlp(x, spec["enc_w"], spec["enc_b"], spec.get("enc_act", "relu"), spec.get("enc_last_relu", False))
+        c = mlp(x, spec["enc_w"], spec["enc_b"], spec.get("enc_act", "relu"), spec.get("enc_last_relu", False),
+                bf16)
         z = shrink(c, spec["lista_thresh"])
         S = np.asarray(spec["lista_S"], np.float32)
         for _ in range(int(spec["lista_loops"])):
-            z = shrink(z @ S + c, spec["lista_thresh"])
+            z = shrink(_mm(z, S, bf16) + c, spec["lista_thresh"])
     out = np.empty((x.shape[0], H, n_assets), np.float32)
     for k in range(H):
-        z = (z @ K).astype(np.float32)
+        z = _mm(z, K, bf16)
         if spec["kind"] == "generic":
             z = norm_fn(z, spec.get("norm_fn", "id"))
-            p = mlp(z, spec["dec_w"], spec["dec_b"], spec.get("dec_act", "relu"), False)
+            p = mlp(z, spec["dec_w"], spec["dec_b"], spec.get("dec_act", "relu"), False, bf16)
         else:
-            p = (z @ lista_decoder_weight(spec["dict"]).T).astype(np.float32)
+            p = _mm(z, lista_decoder_weight(spec["dict"]).T, bf16)
         out[:, k, :] = p[:, :n_assets] * std + mean
     return out
 

@@ -71,7 +71,7 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
          offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
          offsetof(kmpc_rollout_desc, std));
-  printf("%zu\\n", offsetof(kmpc_rollout_desc, obs_ld));
+  printf("%zu %zu\\n", offsetof(kmpc_rollout_desc, obs_ld), offsetof(kmpc_rollout_desc, dtype));
   printf("%zu %zu\\n", sizeof(kmpc_backtest_desc), offsetof(kmpc_backtest_desc, cost_coeff));
   printf("%zu %zu %zu %zu\\n", sizeof(kmpc_mv_desc), offsetof(kmpc_mv_desc, gamma),
          offsetof(kmpc_mv_desc, tol), offsetof(kmpc_mv_desc, return_full_W));
@@ -85,7 +85,7 @@ int main(void) {{
     expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
               ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
-              R.obs_ld.offset,
+              R.obs_ld.offset, R.dtype.offset,
               ctypes.sizeof(Bt), Bt.cost_coeff.offset,
               ctypes.sizeof(Mv), Mv.gamma.offset, Mv.tol.offset, Mv.return_full_W.offset]
     assert [int(x) for x in out] == expect

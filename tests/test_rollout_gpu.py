@@ -129,3 +129,35 @@ def test_panel_rollout_equals_embedded_rollout():
         assert np.abs(y_pan - ref).max() <= 1e-5 * np.abs(ref).max()
     with pytest.raises(ValueError):
         km.rollout_panel(zt, d, T - d, 2, mean, std, H, N)
+
+
+def _oracle_spec(spec):
+    """oracle/rollout.py's dict form of a KoopmanModelSpec."""
+    t = lambda x: None if x is None else x.detach().cpu().numpy()   # noqa: E731
+    d = {"kind": spec.kind, "enc_w": [t(w) for w, _ in spec.encoder], "enc_b": [t(b) for _, b in spec.encoder],
+         "enc_act": spec.enc_act, "enc_last_relu": spec.enc_last_relu, "kmat": t(spec.kmat)}
+    if spec.kind == "generic":
+        d.update(dec_w=[t(w) for w, _ in spec.decoder], dec_b=[t(b) for _, b in spec.decoder],
+                 dec_act=spec.dec_act, norm_fn=spec.norm_fn)
+    else:
+        d.update(dict=t(spec.decoder[0][0]).T.copy(), lista_S=t(spec.lista_S), lista_loops=spec.lista_loops,
+                 lista_thresh=spec.lista_thresh)
+    return d
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "rollout_*.npz"))))
+def test_bf16_rollout_matches_bf16_restatement(path):
+    """KMPC_DTYPE_BF16 (BASELINE configs[4]): GEMM operands rounded to bf16 on the bf16 MFMA, fp32
+    accumulation and epilogues. Checked against the numpy restatement with the same operand rounding
+    (tolerance 2e-3 of max|yhat|: summation order, and the rare activation whose fp32 value sits on
+    a bf16 rounding boundary); its deviation from the reference's fp32 yhat is bounded by 5e-2."""
+    g = np.load(path)
+    meta, spec = load_spec(g)
+    km = DeviceKoopman(spec, torch.device("cuda"), dtype="bf16")
+    obs = g["obs"]
+    y = km.rollout(torch.from_numpy(obs).cuda(), g["mean"], g["std"], meta["H"], meta["N"]).cpu().numpy()
+    ref16 = R.rollout(_oracle_spec(spec), obs, meta["H"], meta["N"], g["mean"].astype(np.float32),
+                      g["std"].astype(np.float32), bf16=True)
+    scale = np.abs(ref16).max()
+    assert np.abs(y - ref16).max() <= 2e-3 * scale
+    assert np.abs(y - g["yhat"]).max() <= 5e-2 * np.abs(g["yhat"]).max()
