@@ -446,6 +446,65 @@ struct Reducer {
             periods(c);
         }
     }
+    // per-period sums of a (in place) and the block minimum of mn, sharing one barrier
+    __device__ __forceinline__ double periods_min(double (&a)[HM], double mn) {
+        constexpr int M = pow2_at_least(HM);
+        constexpr int RW = Shared<HM, NWM>::RW;
+        static_assert(RW > M, "a spare reduction slot per wave");
+        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+        double v[M];
+#pragma unroll
+        for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : 0.0;
+        const int slot = wave_reduce_scatter<M>(v);
+        mn = wave_min(mn);
+        double* r = &sh.red[buf][0][0];
+        if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
+        if (lane == 0) r[wv * RW + M] = mn;
+        __syncthreads();
+        double t0[NWM][HM + 1];
+#pragma unroll
+        for (int q = 0; q < NWM; ++q)
+#pragma unroll
+            for (int j = 0; j <= HM; ++j) t0[q][j] = (q == 0 || q < nw) ? r[q * RW + (j < HM ? j : M)] : 0.0;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < HM; ++j) {
+            double s = t0[0][j];
+#pragma unroll
+            for (int q = 1; q < NWM; ++q) s += t0[q][j];
+            a[j] = s;
+        }
+        double m = t0[0][HM];
+#pragma unroll
+        for (int q = 1; q < NWM; ++q)
+            if (q < nw) m = fmin(m, t0[q][HM]);
+        buf ^= 1;
+        return m;
+    }
+    // block sum of s and block maximum of mx, sharing one barrier
+    __device__ __forceinline__ void sum_max(double s, double mx, double& S, double& MX) {
+        constexpr int RW = Shared<HM, NWM>::RW;
+        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+        s = wave_sum(s);
+        mx = wave_max(mx);
+        double* r = &sh.red[buf][0][0];
+        if (lane == 0) { r[wv * RW] = s; r[wv * RW + 1] = mx; }
+        __syncthreads();
+        double ss[NWM], mm[NWM];
+#pragma unroll
+        for (int q = 0; q < NWM; ++q) {
+            ss[q] = (q == 0 || q < nw) ? r[q * RW] : 0.0;
+            mm[q] = (q == 0 || q < nw) ? r[q * RW + 1] : 0.0;
+        }
+        S = ss[0];
+        MX = mm[0];
+#pragma unroll
+        for (int q = 1; q < NWM; ++q) {
+            S += ss[q];
+            if (q < nw) MX = fmax(MX, mm[q]);
+        }
+        buf ^= 1;
+    }
     __device__ __forceinline__ double sum1(double x) {
         const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
         x = wave_sum(x);
@@ -671,8 +730,9 @@ __device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
             dual_residual<HM, NWM>(T, sh, t, rdw, rds);
             r0[t] = -rdw;
             r1[t] = -rds;
-            bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
-                               fmax(fabs(T.rc1[t]), fmax(fabs(T.rc2[t]), fabs(T.rc3[t])))));
+            if (n_refine > 0)   // ||b||_inf only matters when the solve may be refined
+                bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
+                                   fmax(fabs(T.rc1[t]), fmax(fabs(T.rc2[t]), fabs(T.rc3[t])))));
         }
         if (threadIdx.x == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     }
@@ -784,8 +844,7 @@ __device__ __forceinline__ double max_step(const Thread<HM, NWM * WAVE>& T, Shar
             mdw[t] = T.m[t] * T.dw[t];
         }
     }
-    R.periods(mdw);
-    a = R.min1(a);
+    a = R.periods_min(mdw, a);
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         if (t < H) {
@@ -1286,8 +1345,8 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                         rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
                     }
                 }
-                double mu = R.sum1(mu_l);
-                rd = R.max1(rd);
+                double mu;
+                R.sum_max(mu_l, rd, mu, rd);
                 double pr = 0.0;
                 bool domain_ok = true;
                 for (int t = 0; t < H; ++t) {
