@@ -136,6 +136,53 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
     return base, parity
 
 
+def cpu_baseline_serial(sd, mean, std, x_gpu, wp_gpu, H, N, cfg, budget_s):
+    """BASELINE.md §3 item 1, "reference-semantics serial": one window at a time on one core, as
+    the reference's run_backtest drives KoopmanMPCStrategy.rebalance — a torch-CPU batch-1 rollout
+    in the op order of backtest.py:99-121 (full obs-width decode, slice, de-standardize per step)
+    and the float64 C restatement of the solve (oracle/kmpc_oracle.c, single window, no OpenMP)."""
+    from oracle import solver as osolver
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        enc = [(sd[f"encoder.network.{2 * k}.weight"], sd[f"encoder.network.{2 * k}.bias"]) for k in range(3)]
+        K = sd["kmat"]
+        D = sd["decoder.network.0.weight"]
+        mean_t, std_t = torch.tensor(mean), torch.tensor(std)
+        xs = x_gpu[:256].cpu()
+        wps = wp_gpu[:256].cpu().numpy()
+
+        def window(i):
+            with torch.no_grad():
+                z = xs[i:i + 1]
+                for k, (W, b) in enumerate(enc):              # GenericKM.encode (model.py:756-766)
+                    z = torch.nn.functional.linear(z, W, b)
+                    if k < 2:
+                        z = torch.relu(z)
+                ys = []
+                for _ in range(H):                             # backtest.py:107-119
+                    z = z @ K                                  # step_latent (model.py:787-797), norm 'id'
+                    p_ = torch.nn.functional.linear(z, D)      # decode: full obs width (model.py:768-777)
+                    ys.append((p_[..., :N] * std_t + mean_t).numpy().flatten())
+            y = np.array(ys)                                   # backtest.py:121
+            osolver.solve(wps[i], y, cfg.cost_coeff, cfg.max_turnover, cfg.allow_short, max_iter=cfg.max_iter,
+                          tol=cfg.tol, precision="d")
+
+        window(0)
+        t0 = time.perf_counter()
+        n = 0
+        while n < xs.shape[0] and (n < 8 or time.perf_counter() - t0 < budget_s):
+            window(n)
+            n += 1
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(threads)
+    return {"value": n / dt, "unit": "windows/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} windows of rank 0's C3 batch, one at a time: torch-CPU batch-1 rollout "
+                      f"(backtest.py:99-121 op order, full decode) + float64 C solve (oracle/kmpc_oracle.c), "
+                      f"1 thread, {dt:.1f} s"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,6 +295,8 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base
+            line["cpu_baseline_serial"] = cpu_baseline_serial(sd, mean, std, x, wp, H, N, cfg,
+                                                              min(5.0, args.cpu_seconds / 4))
             line["cpu_parity"] = parity
         print(json.dumps(line), flush=True)
     if world > 1:
