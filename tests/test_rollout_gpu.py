@@ -161,3 +161,42 @@ def test_bf16_rollout_matches_bf16_restatement(path):
     scale = np.abs(ref16).max()
     assert np.abs(y - ref16).max() <= 2e-3 * scale
     assert np.abs(y - g["yhat"]).max() <= 5e-2 * np.abs(g["yhat"]).max()
+
+
+def test_bf16_lista_rollout_at_config5_shape():
+    """BASELINE configs[4] shape: LISTAKM (linear We), N = 500 assets, d = 20 (obs 10000), latent 512,
+    10 LISTA loops, H = 20, bf16 MFMA rollout against the bf16-operand restatement (random weights
+    with L = 1.1 ||We||_2^2 as SURVEY §8(d) prescribes, so the LISTA iteration is contractive)."""
+    rng = np.random.default_rng(5)
+    N, d, L, H, B = 500, 20, 512, 20, 64
+    obs_n = N * d
+    We = (rng.standard_normal((L, obs_n)) / np.sqrt(obs_n)).astype(np.float32)
+    lip = 1.1 * np.linalg.norm(We.astype(np.float64), 2) ** 2
+    S = (np.eye(L) - We.astype(np.float64) @ We.astype(np.float64).T / lip).astype(np.float32)
+    q, _ = np.linalg.qr(rng.standard_normal((L, L)))
+    K = (0.95 * q).astype(np.float32)
+    D = rng.standard_normal((L, obs_n)).astype(np.float32)
+    Dn = (D / np.maximum(np.linalg.norm(D, axis=1, keepdims=True), 1e-4)).astype(np.float32)
+    thr = 5e-3 / lip
+    spec = KoopmanModelSpec(kind="lista", encoder=[(torch.from_numpy(We / np.float32(lip)), None)],
+                            kmat=torch.from_numpy(K), decoder=[(torch.from_numpy(Dn.T.copy()), None)],
+                            lista_S=torch.from_numpy(S), lista_loops=10, lista_thresh=float(thr))
+    obs = rng.standard_normal((B, obs_n)).astype(np.float32)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    km = DeviceKoopman(spec, torch.device("cuda"), dtype="bf16")
+    y = km.rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    ref16 = R.rollout(_oracle_spec(spec), obs, H, N, mean, std, bf16=True)
+    assert y.shape == (B, H, N)
+    # fp32 chain first: the same kernels and data path, exact fp32 products -> summation order only
+    y32 = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    ref32 = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
+    assert np.abs(y32 - ref32).max() <= 1e-4 * np.abs(ref32).max()
+    # bf16 chain: 30 dependent roundings of the state to bf16 (10 LISTA loops, 20 K steps); a
+    # summation-order difference of ~1e-6 flips an occasional element's rounding (1 bf16 ulp =
+    # 2^-8 relative) and the flips propagate — measured ~4e-3 normwise against the bf16-operand
+    # restatement. Bars: 1e-2 normwise, 2^-5 of the decoded scale elementwise; and within 5e-2
+    # (normwise) of the fp32 result.
+    dec = ref16 - mean
+    assert np.linalg.norm(y - ref16) <= 1e-2 * np.linalg.norm(dec)
+    assert np.abs(y - ref16).max() <= 2 ** -5 * np.abs(dec).max()
+    assert np.linalg.norm(y - ref32) <= 5e-2 * np.linalg.norm(ref32 - mean)
