@@ -289,6 +289,7 @@ struct Shared {
     double rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     double t_adw[HM], t_sds[HM], t_sdw[HM];
+    double best_rw[HM], best_l1[HM];   // per-period R.w and ||w_t - w_{t-1}||_1 of the best iterate
     int flag;
 };
 
@@ -444,6 +445,78 @@ struct Reducer {
         } else {
             periods(a, b);
             periods(c);
+        }
+    }
+    // Period totals for their owner only: thread t < HM receives the block totals of period t of
+    // NA arrays flattened in v (array k at slots k*HM .. k*HM+HM-1); other threads get garbage.
+    // No broadcast of all M totals into every lane (the residual / factor / tail consumers are the
+    // HM per-period threads).
+    template <int M, int NA>
+    __device__ __forceinline__ void own_slots(double (&v)[M], double (&out)[NA]) {
+        static_assert(NA * HM <= M && M <= 64, "slots");
+        constexpr int RW = Shared<HM, NWM>::RW;
+        static_assert(RW >= M, "reduction row");
+        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+        const int slot = wave_reduce_scatter<M>(v);
+        double* r = &sh.red[buf][0][0];
+        if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
+        __syncthreads();
+        const int t = threadIdx.x < HM ? threadIdx.x : 0;
+        double tmp[NWM][NA];
+#pragma unroll
+        for (int q = 0; q < NWM; ++q)
+#pragma unroll
+            for (int k = 0; k < NA; ++k) tmp[q][k] = (q == 0 || q < nw) ? r[q * RW + k * HM + t] : 0.0;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < NA; ++k) {
+            double sum = tmp[0][k];
+#pragma unroll
+            for (int q = 1; q < NWM; ++q) sum += tmp[q][k];
+            out[k] = sum;
+        }
+        buf ^= 1;
+    }
+    __device__ __forceinline__ double own1(const double (&a)[HM]) {
+        constexpr int M = pow2_at_least(HM);
+        double v[M], o[1];
+#pragma unroll
+        for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : 0.0;
+        own_slots<M, 1>(v, o);
+        return o[0];
+    }
+    __device__ __forceinline__ void own3(const double (&a)[HM], const double (&b)[HM], const double (&c)[HM],
+                                         double (&out)[4]) {
+        constexpr int M = pow2_at_least(3 * HM);
+        static_assert(M <= 64, "own3");
+        double v[M], o[3];
+#pragma unroll
+        for (int t = 0; t < M; ++t)
+            v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : (t < 3 * HM ? c[t - 2 * HM] : 0.0));
+        own_slots<M, 3>(v, o);
+        out[0] = o[0]; out[1] = o[1]; out[2] = o[2]; out[3] = 0.0;
+    }
+    // four [HM] arrays (two reductions when 4 HM > 64)
+    __device__ __forceinline__ void own4(const double (&a)[HM], const double (&b)[HM], const double (&c)[HM],
+                                         const double (&d)[HM], double (&out)[4]) {
+        constexpr int M4 = pow2_at_least(4 * HM);
+        if constexpr (M4 <= 64) {
+            double v[M4];
+#pragma unroll
+            for (int t = 0; t < M4; ++t)
+                v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : (t < 3 * HM ? c[t - 2 * HM] : (t < 4 * HM ? d[t - 3 * HM] : 0.0)));
+            own_slots<M4, 4>(v, out);
+        } else {
+            constexpr int M2 = pow2_at_least(2 * HM);
+            double v[M2], o[2];
+#pragma unroll
+            for (int t = 0; t < M2; ++t) v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : 0.0);
+            own_slots<M2, 2>(v, o);
+            out[0] = o[0]; out[1] = o[1];
+#pragma unroll
+            for (int t = 0; t < M2; ++t) v[t] = t < HM ? c[t] : (t < 2 * HM ? d[t - HM] : 0.0);
+            own_slots<M2, 2>(v, o);
+            out[2] = o[0]; out[3] = o[1];
         }
     }
     // per-period sums of a (in place) and the block minimum of mn, sharing one barrier
@@ -806,12 +879,10 @@ __device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
     double sds[HM];
 #pragma unroll
     for (int t = 0; t < HM; ++t) sds[t] = (T.act && t < H) ? T.ds[t] : 0.0;
-    R.periods(sds);
+    const double st_own = R.own1(sds);
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
-        double st = 0.0;
-#pragma unroll
-        for (int k = 0; k < HM; ++k) if (k == t) st = sds[k];
+        const double st = st_own;
         const bool on = T.ht && t < H;
         sh.dz4[t] = on ? -st + sh.rg4[t] : 0.0;
         sh.dl4[t] = on ? (sh.b5[t] + sh.l4[t] * st) * sh.iz4[t] : 0.0;
@@ -915,12 +986,10 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
         T.iz2.set(t, iz2);
         T.iz3.set(t, iz3);
     }
-    R.periods(sp);
+    const double st_own = R.own1(sp);
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
-        double st = 0.0;
-#pragma unroll
-        for (int k = 0; k < HM; ++k) if (k == t) st = sp[k];
+        const double st = st_own;
         const double ga = (T.ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
         sh.rho[t] = (T.ht && t < H) ? ga / (1.0 + ga * st) : 0.0;
         sh.sr[t] = sqrt(sh.rho[t]);
@@ -1289,12 +1358,10 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 T.l1[t] = (on && T.hw) ? 1.0 : 0.0;
                 T.l2[t] = T.l3[t] = (on && T.hs) ? 1.0 : 0.0;
             }
-            R.periods(ss0);
+            const double st0 = R.own1(ss0);
             if (threadIdx.x < HM) {
                 const int t = threadIdx.x;
-                double st = 0.0;
-#pragma unroll
-                for (int k = 0; k < HM; ++k) if (k == t) st = ss0[k];
+                const double st = st0;
                 sh.z4[t] = (T.ht && t < H) ? fmax(T.tau - st, 0.5 * T.tau) : 1.0;
                 sh.l4[t] = (T.ht && t < H) ? 1.0 : 0.0;
                 sh.nu[t] = 0.0;
@@ -1308,21 +1375,26 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
             KMPC_PH_START(ph);
             for (it = 0; it < args.max_iter; ++it) {
                 // ---- residuals: den_t = 1 + m.w, 1'w_t - 1, tau - 1's_t - z4 ----
+                double my_rw = 0.0;   // this period thread's R.w total
+                double l1_own[HM];    // this asset's |w_t - w_{t-1}|, reduced only when the iterate is kept
                 {
-                    double mw[HM], sw[HM], ssum[HM];
+                    double mw[HM], sw[HM], ssum[HM], l1n[HM];
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
                         const bool on = T.act && t < H;
                         mw[t] = on ? T.m[t] * T.w[t] : 0.0;
                         sw[t] = on ? T.w[t] : 0.0;
                         ssum[t] = on ? T.s[t] : 0.0;
+                        l1n[t] = on ? fabs(T.w[t] - T.wprev(t)) : 0.0;
                     }
-                    R.periods(mw, sw, ssum);
+                    double o[4];
+                    R.own3(mw, sw, ssum, o);
+#pragma unroll
+                    for (int t = 0; t < HM; ++t) l1_own[t] = l1n[t];
                     if (threadIdx.x < HM) {
                         const int t = threadIdx.x;
-                        double a = 0.0, b2 = 0.0, c2 = 0.0;
-#pragma unroll
-                        for (int k = 0; k < HM; ++k) if (k == t) { a = mw[k]; b2 = sw[k]; c2 = ssum[k]; }
+                        const double a = o[0], b2 = o[1], c2 = o[2];
+                        my_rw = b2 + a;          // sum_i exp(yhat) w = sum w + sum expm1(yhat) w
                         const bool on = t < H;
                         sh.den[t] = 1.0 + a;
                         sh.iden[t] = 1.0 / (1.0 + a);
@@ -1363,7 +1435,17 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 if (!domain_ok || !isfinite(merit)) break;
                 if (merit < best) {
                     best = merit;
-                    best_obj = record_best<HM, NWM>(T, R, wout, yh, args.c, tw);
+                    // the answer is this iterate: W to HBM, its period totals for problem.value
+                    // (evaluated once, after the loop)
+#pragma unroll
+                    for (int t = 0; t < HM; ++t)
+                        if (T.act && t < H && t < tw) wout[t * N + T.i] = T.w[t];
+                    const double l1t = R.own1(l1_own);
+                    if (threadIdx.x < HM) {
+                        sh.best_rw[threadIdx.x] = my_rw;
+                        sh.best_l1[threadIdx.x] = l1t;
+                    }
+                    best_obj = 0.0;
                 } else if (best < 1e-6 && merit > 1e4 * best) {
                     break;   // numerical breakdown after convergence: keep the best iterate
                 }
@@ -1448,6 +1530,13 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                 }
                 __syncthreads();
                 KMPC_PH(ph, 6);
+            }
+            __syncthreads();   // sh.best_* of the best iterate visible
+            if (best < 1e300) {
+                // problem.value (mpc.py:103) at the best iterate: sum_t log(R_t . w_t) - c ||w_t - w_{t-1}||_1
+                double f = 0.0;
+                for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) - args.c * sh.best_l1[t];
+                best_obj = f;
             }
             if (best <= 1e-7) status = KMPC_STATUS_OPTIMAL;
             else if (best <= 1e-4) status = KMPC_STATUS_OPTIMAL_INACCURATE;
