@@ -1571,6 +1571,9 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
         const size_t lds = cold_bytes<HM, 256>();
         if (exact) hipLaunchKernelGGL((ipm_kernel<HM, 256, true>), dim3(a.B), dim3(nt), lds, stream, a);
         else hipLaunchKernelGGL((ipm_kernel<HM, 256, false>), dim3(a.B), dim3(nt), lds, stream, a);
+    } else if (nt <= 512) {
+        // two waves per SIMD: 256 registers per thread (the 1024-thread variant has 128)
+        hipLaunchKernelGGL((ipm_kernel<HM, 512, false>), dim3(a.B), dim3(nt), 0, stream, a);
     } else {
         hipLaunchKernelGGL((ipm_kernel<HM, 1024, false>), dim3(a.B), dim3(nt), 0, stream, a);
     }

@@ -85,7 +85,8 @@ def test_fallback_statuses_on_device():
     assert info == {"status": "infeasible", "value": None}
 
 
-@pytest.mark.parametrize("N,H", [(1, 3), (63, 4), (64, 5), (65, 6), (129, 2), (300, 7), (20, 12)])
+@pytest.mark.parametrize("N,H", [(1, 3), (63, 4), (64, 5), (65, 6), (129, 2), (300, 7), (20, 12),
+                                 (500, 20), (700, 3)])   # 512- and 1024-thread variants
 def test_ragged_shapes_match_oracle(N, H):
     rng = np.random.default_rng(N * 31 + H)
     B = 6
