@@ -1522,13 +1522,16 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                         T.s[t] += step * T.ds[t];
                     }
                 }
+                // every thread's max_step ratio test (pass 1) has read sh.z4 / sh.l4 before the
+                // period threads overwrite them; the next reads (period owners, then everyone) sit
+                // behind the next iteration's residual barriers
+                __syncthreads();
                 if (threadIdx.x < HM && (int)threadIdx.x < H) {
                     const int t = threadIdx.x;
                     sh.z4[t] += step * sh.dz4[t];
                     sh.l4[t] += step * sh.dl4[t];
                     sh.nu[t] += step * sh.dnu[t];
                 }
-                __syncthreads();
                 KMPC_PH(ph, 6);
             }
             __syncthreads();   // sh.best_* of the best iterate visible
