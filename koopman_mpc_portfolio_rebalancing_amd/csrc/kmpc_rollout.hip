@@ -101,11 +101,23 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[2][2],
         }
 }
 
+// XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs by linear id,
+// so neighbouring tiles of one row panel of A would land in 8 different L2s. Renumber so that each
+// XCD gets a contiguous run of tiles (same A row panels): id -> (id % 8) * (total / 8) + id / 8.
+__device__ __forceinline__ void xcd_tile(int& m0, int& n0) {
+    const int gx = gridDim.x, total = gridDim.x * gridDim.y;
+    int id = blockIdx.y * gx + blockIdx.x;
+    if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+    m0 = (id / gx) * BM;
+    n0 = (id % gx) * BN;
+}
+
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     __shared__ float As[BM * LDS_STRIDE];
     __shared__ float Bs[BN * LDS_STRIDE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    int m0, n0;
+    xcd_tile(m0, n0);
     const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
     f32x16 acc[2][2];
 #pragma unroll
@@ -178,7 +190,8 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
     __shared__ __bf16 As[BM * LDS_STRIDE_H];
     __shared__ __bf16 Bs[BN * LDS_STRIDE_H];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    int m0, n0;
+    xcd_tile(m0, n0);
     const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
     f32x16 acc[2][2];
 #pragma unroll
