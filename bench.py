@@ -41,7 +41,7 @@ HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 # per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
-PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_solve_pmc.json")
+PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02_solve_pmc.json")
 
 
 def parse():
@@ -261,15 +261,27 @@ def main():
         # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scaled
         # to this launch's windows) and the executed f64 VALU rate of the solve against its peak:
         # the solver is bound by f64 latency / VALU, not by HBM
-        traffic, compute = None, None
+        traffic, f64_rate = None, None
         if os.path.exists(PMC_JSON) and (N, H) == (100, 10):
             pmc = json.load(open(PMC_JSON))
             traffic = (pmc["fetch_bytes_per_window"] + pmc["write_bytes_per_window"]) * B
             if "f64_flops_per_window" in pmc:
-                f64 = pmc["f64_flops_per_window"] * B / (solve_ms * 1e-3)
-                compute = {"bound": "valu_f64", "achieved": f64 / 1e12, "peak": F64_VALU_PEAK / 1e12,
-                           "unit": "TFLOP/s", "frac": f64 / F64_VALU_PEAK,
-                           "flops": "executed f64 VALU FLOPs per window from PMC (profiles/r01_solve_pmc.json)"}
+                f64_rate = pmc["f64_flops_per_window"] * B / (solve_ms * 1e-3)
+        hbm = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK, "traffic": traffic,
+               "algorithmic_bytes_per_window": solve_bytes // B}
+        # The solve kernel is bound by f64 arithmetic issue / latency, not by HBM (it reads each
+        # input once): its roofline is the f64 peak (78.6 TFLOP/s, the same for the
+        # f64 MFMA and the f64 VALU on MI355X), against the executed f64 FLOPs of the launch (PMC
+        # per-window count x windows / HIP-event launch time). The HBM figure stays beside it.
+        if f64_rate is not None:
+            roof = {"bound": "mfma", "achieved": f64_rate / 1e12, "peak": F64_VALU_PEAK / 1e12,
+                    "unit": "TFLOP/s", "frac": f64_rate / F64_VALU_PEAK, "traffic": traffic,
+                    "dtype": "f64", "kernel": "kmpc_solve (ipm_kernel<10,128,true,7>)", "launch_ms": solve_ms,
+                    "flops": "executed f64 FLOPs per window from PMC (profiles/r02_solve_pmc.json), "
+                             "pipe: f64 VALU (no f64 MFMA use; same 78.6 TFLOP/s peak)"}
+        else:
+            roof = dict(hbm, kernel="kmpc_solve", launch_ms=solve_ms)
         roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
                                 + H * (L * L + L * N))
         line = {
@@ -281,11 +293,8 @@ def main():
                                    f"GenericKM enc [{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
                        "windows_per_gpu": B, "global_windows_per_step": world * B,
                        "parallelism": f"windows sharded over {world} GPU(s), RCCL gather of W0"},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": "kmpc_solve (ipm_kernel<10,128,true>)",
-                         "algorithmic_bytes_per_window": solve_bytes // B, "launch_ms": solve_ms},
-            "compute_roofline": compute,
+            "roofline": roof,
+            "hbm_roofline": hbm,
             "kernels": {"rollout_ms": roll_ms, "solve_ms": solve_ms,
                         "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
                         "rollout_mfma_frac": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK},

@@ -20,6 +20,16 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
+    // H == 5 / 10 with N <= 128 in the two common constraint cases: constant-case kernels
+    if (a.H == 10 || a.H == 5) {
+        const int rc = a.H == 10 ? launch_ipm_case<10>(a, stream) :
+#ifndef KMPC_DEV_ONLY_H10
+                                   launch_ipm_case<5>(a, stream);
+#else
+                                   KMPC_ERR_UNSUPPORTED;
+#endif
+        if (rc != KMPC_ERR_UNSUPPORTED) return rc;
+    }
 #ifndef KMPC_DEV_ONLY_H10
     if (a.H <= 2) return launch_ipm<2>(a, stream);
     if (a.H <= 5) return launch_ipm<5>(a, stream);

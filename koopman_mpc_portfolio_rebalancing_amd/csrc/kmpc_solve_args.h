@@ -21,5 +21,8 @@ struct SolveArgs {
 // ipm_kernel launchers, one translation unit per compile-time horizon bound HM (kmpc_solve_h*.hip)
 template <int HM>
 int launch_ipm(const SolveArgs& a, hipStream_t stream);
+// constant-case kernels (kmpc_solve_h*_case.hip); KMPC_ERR_UNSUPPORTED if the case has none
+template <int HM>
+int launch_ipm_case(const SolveArgs& a, hipStream_t stream);
 
 }  // namespace kmpc

@@ -1,0 +1,7 @@
+// kmpc_solve_h5_case.hip — constant-case ipm_kernel instantiations for H == 5 (see
+// kmpc_solve_kernel.h, launch_ipm_case).
+#include "kmpc_solve_kernel.h"
+
+namespace kmpc {
+template int launch_ipm_case<5>(const SolveArgs& a, hipStream_t stream);
+}  // namespace kmpc

@@ -293,11 +293,29 @@ struct Shared {
     int flag;
 };
 
-template <int HM, int MAXT>
-struct Thread {
+// Constraint case of a launch: bit 0 no-short (w >= 0), bit 1 turnover terms (c > 0 or tau > 0),
+// bit 2 turnover cap (tau > 0). FL >= 0 fixes the case at compile time (every predicate on it
+// folds away: no selects, no divergent branches); FL = -1 reads it from the launch arguments.
+template <int FL>
+struct Case {
+    static constexpr bool hw = (FL & 1) != 0, hs = (FL & 2) != 0, ht = (FL & 4) != 0;
+    __device__ __forceinline__ void set_case(bool, bool, bool) {}
+};
+template <>
+struct Case<-1> {
+    bool hw, hs, ht;
+    __device__ __forceinline__ void set_case(bool a, bool b, bool c) { hw = a; hs = b; ht = c; }
+};
+__host__ __device__ constexpr int case_of(bool hw, bool hs, bool ht) { return (hw ? 1 : 0) | (hs ? 2 : 0) | (ht ? 4 : 0); }
+
+template <int HM, int MAXT, int FL = -1>
+struct Thread : Case<FL> {
+    using Case<FL>::hw;
+    using Case<FL>::hs;
+    using Case<FL>::ht;
     static constexpr bool L = cold_in_lds<HM, MAXT>();
     int H, N, i;
-    bool act, hw, hs, ht;
+    bool act;
     double c, tau, sig, isig, irsig, wpi;
     // state
     double w[HM], s[HM], l1[HM], l2[HM], l3[HM], m[HM];
@@ -631,8 +649,8 @@ __device__ __forceinline__ double to_bound(double v, double dv, double a) {
 }
 
 // Dual residuals of the current iterate (rows 1-2) at period t.
-template <int HM, int NWM>
-__device__ __forceinline__ void dual_residual(const Thread<HM, NWM * WAVE>& T, const Shared<HM, NWM>& sh, int t,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ void dual_residual(const TH& T, const Shared<HM, NWM>& sh, int t,
                                               double& rdw, double& rds) {
     const double eta = T.l3[t] - T.l2[t];
     const double etan = (t + 1 < HM && t + 1 < T.H) ? T.l3[t + 1] - T.l2[t + 1] : 0.0;
@@ -643,8 +661,8 @@ __device__ __forceinline__ void dual_residual(const Thread<HM, NWM * WAVE>& T, c
 // Solve the Newton system (oracle/kmpc_oracle.c:lsolve) for rhs rows (bw, bs, [-rc if with_c],
 // sh.lb5, sh.lb6), in place: on return bw = dw, bs = ds (and q in sh.bs; the budget multipliers
 // are q[2H..3H)). In-place arrays keep the register footprint of the solve to four [HM] arrays.
-template <int HM, int NWM>
-__device__ __forceinline__ void lsolve(const Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
                                        double (&bw)[HM], double (&bs)[HM], bool with_c) {
     constexpr int KM = 3 * HM;
     const int H = T.H;
@@ -779,8 +797,8 @@ __device__ __forceinline__ void lsolve(const Thread<HM, NWM * WAVE>& T, Shared<H
 // Full Newton direction for the current rc targets, with adaptive iterative refinement against
 // the unreduced system (one lsolve body for the solve and its refinements).
 // On exit: T.dw, T.ds, sh.dnu, sh.dz4, sh.dl4.
-template <int HM, int NWM>
-__device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
                                        int n_refine) {
     const int H = T.H;
     PhaseClock np;
@@ -892,8 +910,8 @@ __device__ __forceinline__ void newton(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
 }
 
 // Largest step for the current direction (before the caller's fraction-to-boundary).
-template <int HM, int NWM>
-__device__ __forceinline__ double max_step(const Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R) {
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R) {
     const int H = T.H;
     double a = 1e300, mdw[HM];
     double DL1[HM], DL2[HM], DL3[HM];
@@ -926,8 +944,8 @@ __device__ __forceinline__ double max_step(const Thread<HM, NWM * WAVE>& T, Shar
     return a;
 }
 
-template <int HM, int NWM>
-__device__ __forceinline__ double complementarity(const Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ double complementarity(const TH& T, Shared<HM, NWM>& sh,
                                                   Reducer<HM, NWM>& R, double a) {
     const int H = T.H;
     double acc = 0.0;
@@ -957,8 +975,8 @@ __device__ __forceinline__ double complementarity(const Thread<HM, NWM * WAVE>& 
 //   G_jl = sum_i c_j c_l (Qi[tj][tl] - [vj] Qi[tj-1][tl] - [vl] Qi[tj][tl-1] + [vj vl] Qi[tj-1][tl-1])
 // with c = alpha_t (a), eps_t (v), 1 (budget); Q^{-1} columns from the LDL^T:
 //   Qi[c][c] = dq_c,  Qi[r][c] = Lr_{r+1} Qi[r+1][c]  (r < c).
-template <int HM, int NWM>
-__device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
                                       PhaseClock& ph) {
     constexpr int KM = 3 * HM;
     constexpr int MC = Shared<HM, NWM>::MC;
@@ -1245,8 +1263,8 @@ __device__ __forceinline__ bool factor(Thread<HM, NWM * WAVE>& T, Shared<HM, NWM
 
 // Write the current iterate as the answer (W[0] or W) and return problem.value at it:
 // sum_t log(w_t . exp(y_t)) - c sum_t ||w_t - w_{t-1}||_1  (mpc.py:66-103).
-template <int HM, int NWM>
-__device__ __forceinline__ double record_best(const Thread<HM, NWM * WAVE>& T, Reducer<HM, NWM>& R, double* wout,
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM>& R, double* wout,
                                               const float* yh, double c, int tw) {
     const int H = T.H, N = T.N;
     double rw[HM], l1n[HM];
@@ -1268,7 +1286,7 @@ __device__ __forceinline__ double record_best(const Thread<HM, NWM * WAVE>& T, R
 }
 
 // EXACT: H == HM known at compile time (all period predicates fold away).
-template <int HM, int MAXT, bool EXACT>
+template <int HM, int MAXT, bool EXACT, int FL = -1>
 __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
     static_assert(3 * HM <= WAVE, "Schur system must fit one wave");
     constexpr int NWM = MAXT / WAVE;
@@ -1276,15 +1294,13 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
     const int b = blockIdx.x;
     const int nw = blockDim.x / WAVE;
     Reducer<HM, NWM> R(sh, nw);
-    Thread<HM, MAXT> T;
+    Thread<HM, MAXT, FL> T;
     T.bind_cold();
     T.H = EXACT ? HM : args.H;
     T.N = args.N;
     T.i = threadIdx.x;
     T.act = T.i < args.N;
-    T.hw = !args.allow_short;
-    T.hs = (args.c > 0.0) || (args.tau > 0.0);
-    T.ht = args.tau > 0.0;
+    T.set_case(!args.allow_short, (args.c > 0.0) || (args.tau > 0.0), args.tau > 0.0);
     T.tau = args.tau;
     const int H = T.H, N = T.N;
     const double* wp = args.wp + (size_t)b * N;   // (H is a compile-time constant when EXACT)
@@ -1562,25 +1578,40 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
     }
 }
 
+template <int HM, int MAXT, bool EXACT, int FL>
+int launch_one(const SolveArgs& a, int nt, hipStream_t stream) {
+    const size_t lds = cold_bytes<HM, MAXT>();
+    hipLaunchKernelGGL((ipm_kernel<HM, MAXT, EXACT, FL>), dim3(a.B), dim3(nt), lds, stream, a);
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+// Generic launcher (constraint case read at run time): one workgroup of 64 * ceil(N / 64) threads
+// per window. The 64-thread variant sizes its LDS for one wave, so four one-wave windows share a
+// CU (the 128-thread variant's LDS admits two windows per CU).
 template <int HM>
 int launch_ipm(const SolveArgs& a, hipStream_t stream) {
     const int nt = WAVE * ((a.N + WAVE - 1) / WAVE);
     const bool exact = a.H == HM;
-    if (nt <= 128) {
-        const size_t lds = cold_bytes<HM, 128>();
-        if (exact) hipLaunchKernelGGL((ipm_kernel<HM, 128, true>), dim3(a.B), dim3(nt), lds, stream, a);
-        else hipLaunchKernelGGL((ipm_kernel<HM, 128, false>), dim3(a.B), dim3(nt), lds, stream, a);
-    } else if (nt <= 256) {
-        const size_t lds = cold_bytes<HM, 256>();
-        if (exact) hipLaunchKernelGGL((ipm_kernel<HM, 256, true>), dim3(a.B), dim3(nt), lds, stream, a);
-        else hipLaunchKernelGGL((ipm_kernel<HM, 256, false>), dim3(a.B), dim3(nt), lds, stream, a);
-    } else if (nt <= 512) {
-        // two waves per SIMD: 256 registers per thread (the 1024-thread variant has 128)
-        hipLaunchKernelGGL((ipm_kernel<HM, 512, false>), dim3(a.B), dim3(nt), 0, stream, a);
-    } else {
-        hipLaunchKernelGGL((ipm_kernel<HM, 1024, false>), dim3(a.B), dim3(nt), 0, stream, a);
-    }
-    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+    if (nt <= 64) return exact ? launch_one<HM, 64, true, -1>(a, nt, stream) : launch_one<HM, 64, false, -1>(a, nt, stream);
+    if (nt <= 128) return exact ? launch_one<HM, 128, true, -1>(a, nt, stream) : launch_one<HM, 128, false, -1>(a, nt, stream);
+    if (nt <= 256) return exact ? launch_one<HM, 256, true, -1>(a, nt, stream) : launch_one<HM, 256, false, -1>(a, nt, stream);
+    // two waves per SIMD: 256 registers per thread (the 1024-thread variant has 128)
+    if (nt <= 512) return launch_one<HM, 512, false, -1>(a, nt, stream);
+    return launch_one<HM, 1024, false, -1>(a, nt, stream);
+}
+
+// Constant-case launcher (H == HM, N <= 128): the constraint case is a template argument, so every
+// predicate on it folds away. Cases: 7 = no short + cost + cap (the benchmark's), 1 = no short
+// only (c = tau = 0: the simplex program of BASELINE configs[1]). Returns KMPC_ERR_UNSUPPORTED for
+// any other case (the caller then uses launch_ipm).
+template <int HM>
+int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
+    const int nt = WAVE * ((a.N + WAVE - 1) / WAVE);
+    const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
+    if (a.H != HM || nt > 128) return KMPC_ERR_UNSUPPORTED;
+    if (fl == 7) return nt <= 64 ? launch_one<HM, 64, true, 7>(a, nt, stream) : launch_one<HM, 128, true, 7>(a, nt, stream);
+    if (fl == 1) return nt <= 64 ? launch_one<HM, 64, true, 1>(a, nt, stream) : launch_one<HM, 128, true, 1>(a, nt, stream);
+    return KMPC_ERR_UNSUPPORTED;
 }
 
 }  // namespace kmpc

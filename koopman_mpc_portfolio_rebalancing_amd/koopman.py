@@ -134,7 +134,7 @@ class DeviceKoopman:
         self.S = up(spec.lista_S)
         if len(self.enc) > _lib.KMPC_MAX_LAYERS or len(self.dec) > _lib.KMPC_MAX_LAYERS:
             raise _lib.KmpcError("too many layers for kmpc_mlp")
-        self._ws = None
+        self._ws = {}   # workspace per HIP stream (kmpc.h: calls are stream-ordered)
 
     @property
     def latent(self) -> int:
@@ -176,9 +176,19 @@ class DeviceKoopman:
         return d
 
     def _workspace(self, nbytes: int) -> torch.Tensor:
-        if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
-        return self._ws
+        """Scratch for one call, private to the caller's current stream: calls issued on
+        different streams never share (and overwrite) a workspace. torch's caching allocator
+        keeps each buffer alive for its stream."""
+        key = _lib.stream_handle(self.device) or 0
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def _check_obs(self, x: torch.Tensor) -> None:
+        if x.dim() != 2 or x.shape[1] != self.obs_size:
+            raise ValueError(f"obs must be [B, {self.obs_size}], got {tuple(x.shape)}")
 
     def _stats(self, mean, std, N):
         m = torch.as_tensor(mean, dtype=torch.float32, device=self.device).reshape(-1)[:N].contiguous()
@@ -189,9 +199,8 @@ class DeviceKoopman:
         """yhat [B, H, N] float32 (predicted de-standardized log-returns) for obs [B, obs_size]."""
         _lib.require_gpu(obs)
         x = obs.to(self.device, torch.float32).contiguous()
+        self._check_obs(x)
         B = x.shape[0]
-        if x.shape[1] != self.obs_size:
-            raise ValueError(f"obs width {x.shape[1]} != model observation size {self.obs_size}")
         m, s = self._stats(mean, std, n_assets)
         y = torch.empty((B, horizon, n_assets), dtype=torch.float32, device=self.device)
         d = self.rollout_desc(B, horizon, n_assets, m, s)
@@ -248,9 +257,14 @@ class DeviceKoopman:
         from .mpc import _solve_desc
         _lib.require_gpu(obs)
         x = obs.to(self.device, torch.float32).contiguous()
+        self._check_obs(x)
         B = x.shape[0]
         H = int(mpc_config.horizon)
         wp = w_prev.to(self.device, torch.float64).contiguous()
+        if wp.shape != (B, int(n_assets)):
+            raise ValueError(f"w_prev must be [{B}, {int(n_assets)}], got {tuple(wp.shape)}")
+        if not 0 < int(n_assets) <= self.obs_size:
+            raise ValueError(f"n_assets {n_assets} must be in 1..obs_size ({self.obs_size})")
         m, s = self._stats(mean, std, n_assets)
         rd = self.rollout_desc(B, H, n_assets, m, s)
         sd = _solve_desc(B, n_assets, H, mpc_config, return_full)
