@@ -43,29 +43,33 @@ size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_des
     size_t bytes = 0;
     if (rdesc) bytes += kmpc::rollout_workspace_bytes(rdesc);
     if (rdesc && sdesc) bytes += align256(sizeof(float) * (size_t)rdesc->B * rdesc->H * rdesc->N);
+    if (sdesc && check_solve(sdesc) == KMPC_OK) bytes += align256(kmpc::solve_workspace_bytes(sdesc));
     return bytes;
 }
 
 int kmpc_solve(const kmpc_solve_desc* desc, const float* yhat, const double* w_prev, double* w_out,
                int* status, double* obj, int* iters, void* workspace, size_t ws_bytes,
                void* stream) {
-    (void)workspace; (void)ws_bytes;
     int rc = check_solve(desc);
     if (rc) return rc;
     if (desc->B == 0) return KMPC_OK;
     if (!yhat || !w_prev || !w_out || !status || !obj) return KMPC_ERR_INVALID;
-    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, (hipStream_t)stream);
+    if (ws_bytes < kmpc::solve_workspace_bytes(desc)) return KMPC_ERR_WORKSPACE;
+    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, workspace, ws_bytes,
+                              (hipStream_t)stream);
 }
 
 /* Debug entry (not part of include/kmpc.h): kmpc_solve plus a per-iteration trace of problem 0,
    trace[4 * it + {0,1,2,3}] = (mu, dual residual, primal residual, step length). */
 int kmpc_solve_trace(const kmpc_solve_desc* desc, const float* yhat, const double* w_prev,
                      double* w_out, int* status, double* obj, int* iters, double* trace,
-                     void* stream) {
+                     void* workspace, size_t ws_bytes, void* stream) {
     int rc = check_solve(desc);
     if (rc) return rc;
     if (desc->B == 0) return KMPC_OK;
-    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, (hipStream_t)stream, trace);
+    if (ws_bytes < kmpc::solve_workspace_bytes(desc)) return KMPC_ERR_WORKSPACE;
+    return kmpc::solve_launch(desc, yhat, w_prev, w_out, status, obj, iters, workspace, ws_bytes,
+                              (hipStream_t)stream, trace);
 }
 
 int kmpc_rollout(const kmpc_rollout_desc* desc, const float* obs, float* yhat, void* workspace,
@@ -82,11 +86,13 @@ int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc, co
     if (rdesc->B != sdesc->B || rdesc->N != sdesc->N || rdesc->H != sdesc->H) return KMPC_ERR_INVALID;
     if (ws_bytes < kmpc_workspace_bytes(rdesc, sdesc)) return KMPC_ERR_WORKSPACE;
     const size_t rbytes = kmpc::rollout_workspace_bytes(rdesc);
+    const size_t ybytes = align256(sizeof(float) * (size_t)rdesc->B * rdesc->H * rdesc->N);
     float* y = yhat ? yhat : (float*)((char*)workspace + rbytes);
     rc = kmpc::rollout_launch(rdesc, obs, y, workspace, rbytes, (hipStream_t)stream);
     if (rc) return rc;
     if (sdesc->B == 0) return KMPC_OK;
-    return kmpc::solve_launch(sdesc, y, w_prev, w_out, status, obj, iters, (hipStream_t)stream);
+    return kmpc::solve_launch(sdesc, y, w_prev, w_out, status, obj, iters, (char*)workspace + rbytes + ybytes,
+                              ws_bytes - rbytes - ybytes, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -7,8 +7,9 @@
 namespace kmpc {
 
 // kmpc_solve.hip
+size_t solve_workspace_bytes(const kmpc_solve_desc* d);
 int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_prev, double* w_out,
-                 int* status, double* obj, int* iters, hipStream_t stream,
+                 int* status, double* obj, int* iters, void* ws, size_t ws_bytes, hipStream_t stream,
                  double* trace = nullptr);
 
 // kmpc_backtest.hip

@@ -21,6 +21,9 @@ struct SolveArgs {
 // ipm_kernel launchers, one translation unit per compile-time horizon bound HM (kmpc_solve_h*.hip)
 template <int HM>
 int launch_ipm(const SolveArgs& a, hipStream_t stream);
+// large-window kernel (kmpc_solve_big.hip): workspace it needs, and the launch
+size_t big_ws_bytes(const SolveArgs& a);
+int big_launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream);
 // constant-case kernels (kmpc_solve_h*_case.hip); KMPC_ERR_UNSUPPORTED if the case has none
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream);

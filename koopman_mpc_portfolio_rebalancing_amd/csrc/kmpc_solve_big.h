@@ -1,0 +1,1065 @@
+#pragma once
+// kmpc_solve_big.h — batched MPC solve for large windows (replaces solve_mpc_log_utility,
+// mpc.py:27-117, for N > 256 assets or H > 10 periods): the same program and the same Mehrotra
+// predictor-corrector interior point as ipm_kernel / oracle/kmpc_oracle.c (same reductions,
+// refinement rule, step rule, status and fallback), laid out for windows whose state does not fit
+// one CU.
+//
+// Why a second kernel: a window's IPM state is ~17 arrays of H x N doubles (1.4 MB at N = 500,
+// H = 20, BASELINE configs[4]); ipm_kernel keeps it in registers (one asset per lane, every period
+// in VGPRs) and past 128 assets or 10 periods spills it to scratch. Here the state lives in a
+// per-window slab of the caller's workspace, [array][t][i] with the assets contiguous, so every
+// access is one coalesced wave load; each phase streams only the arrays it needs, and the
+// slack-derived quantities (reciprocals, P, the s-elimination coefficients) are recomputed from the
+// state instead of stored. The solve is bound by that HBM / Infinity-Cache stream.
+//
+// Layout: one workgroup per window, one asset per thread (blockDim = 64 ceil(N / 64) <= 1024), a
+// persistent grid of min(B, MAX_SLOTS) workgroups walks the windows (workspace = slots x slab).
+// Period loops are runtime loops with scalar carries (no per-period register arrays: small code,
+// bounded registers); per-period block sums are wave butterflies (permlane / DPP) per period into
+// LDS slots, then one pass over the waves. Per-period scalars, the Schur matrix and the reduction
+// slots sit in LDS (~60 KB).
+//
+// Schur (Woodbury) matrix on the matrix cores. G = I' + sum_i Z_i^T Q_i^{-1} Z_i with Q_i the
+// per-asset tridiagonal (in t) and Z_i = [v_t | a_t | 1_t] columns (index j = 3t + type, types
+// v, a, 1). The inverse of a tridiagonal is semiseparable: Q^{-1}[r][c] = dq_c prod_{r<k<=c} Lr_k =
+// g_r beta_c (r <= c) with g = 1 / pi, beta = dq pi, pi_t = prod_{k<=t} Lr_k. So for j <= l (index
+// order) every entry of an asset's contribution is a product Lgen_i[j] * Rgen_i[l], and the sum over
+// assets is the GEMM Lgen^T Rgen: v_mfma_f64_16x16x4_f64 with the assets as the K dimension (exact
+// f64 products, no cross-lane reduction). The one entry whose product form cancels
+// catastrophically, (v_t, v_t), is summed directly. Lr is clamped at 1e-14 (pi stays in the normal
+// range over 21 periods) and pi is centred (pi * 2^(-e/2), pi_H ~ 2^e); the clamp changes Q^{-1}
+// entries only where they are already below 1e-14 of the diagonal, i.e. at f64 rounding level.
+#include "kmpc_solve_kernel.h"
+
+namespace kmpc {
+namespace big {
+
+constexpr int KP = 64;             // padded Schur width (3 HM <= 63)
+constexpr int LDG = 65;            // LDS row stride of G / L (conflict-free row and column reads)
+constexpr int NWX = 16;            // max waves per window (1024 threads)
+constexpr int MAX_SLOTS = 512;     // windows in flight = workspace slabs
+constexpr double LR_FLOOR = 1e-14;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// per-(t, i) arrays of a window's slab (assets contiguous)
+enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
+             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, N_ARR };
+
+__host__ __device__ inline size_t slab_doubles(int HM, int NP) {
+    return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
+}
+
+struct BigArgs {
+    SolveArgs s;
+    double* ws;      // slots x slab doubles
+    size_t slab;     // doubles per slab
+    int NP;          // padded asset count (blockDim)
+};
+
+template <int HM>
+struct BigShared {
+    double G[KP * LDG];          // Schur matrix (lower triangle), then L (unit lower, strictly below)
+    double gid[KP];              // 1 / D of G = L D L^T
+    double q[KP];                // Schur solution (period-major index 3t + type)
+    double tot[3 * KP];          // block-reduction totals
+    double red[NWX][3 * KP];     // per-wave partial slots of a period reduction
+    double sc[2][NWX][2];        // per-wave partials of scalar reductions (alternating)
+    double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
+    double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
+    double rw[HM], best_rw[HM], best_l1[HM], px[HM], adw[HM], sds[HM], sdw[HM];
+    int flag;
+};
+
+// state of one (t, i) with its slack-derived quantities (recomputed, never stored)
+struct St {
+    double w, s, d, l1, l2, l3, m;
+    double iw, iz2, iz3, P, bma;
+};
+
+// 1 / x to ~1 ulp: v_rcp_f64 and two Newton steps (no division sequence)
+__device__ __forceinline__ double rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+}
+
+template <int HM, int FL>
+struct Win {
+    const SolveArgs& a;
+    BigShared<HM>& sh;
+    double* g;       // this window's slab
+    int N, H, NP, nw, i;
+    bool act;        // this thread's asset exists
+    Case<FL> cs;
+    double tau, isig, irsig, cs_c, wpi;
+    int sbuf;
+
+    __device__ __forceinline__ bool hw() const { return cs.hw; }
+    __device__ __forceinline__ bool hs() const { return cs.hs; }
+    __device__ __forceinline__ bool ht() const { return cs.ht; }
+    __device__ __forceinline__ double& at(int arr, int t) const { return g[((size_t)arr * HM + t) * NP + i]; }
+    __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
+    __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
+    __device__ __forceinline__ double wprev(int t) const { return t ? at(A_W, t - 1) : wpi; }
+
+    __device__ __forceinline__ St st(int t, double wp) const {
+        St e;
+        e.w = at(A_W, t);
+        e.s = at(A_S, t);
+        e.l1 = at(A_L1, t);
+        e.l2 = at(A_L2, t);
+        e.l3 = at(A_L3, t);
+        e.m = at(A_M, t);
+        e.d = e.w - wp;
+        e.iw = hw() ? rcp(e.w) : 0.0;
+        if (hs()) {
+            e.iz2 = rcp(e.s - e.d);
+            e.iz3 = rcp(e.s + e.d);
+            const double al = e.l2 * e.iz2, be = e.l3 * e.iz3;
+            e.P = rcp(al + be);
+            e.bma = be - al;
+        } else {
+            e.iz2 = e.iz3 = e.P = e.bma = 0.0;
+        }
+        return e;
+    }
+    // dual residual rows (1)-(2) at period t (ipm_kernel dual_residual); l2n / l3n of period t + 1
+    __device__ __forceinline__ void dres(int t, const St& e, double l2n, double l3n, double& rdw, double& rds) const {
+        rdw = -e.m * sh.iden[t] * isig - (e.l1 + (e.l3 - e.l2) - (l3n - l2n)) + sh.nu[t];
+        rds = hs() ? cs_c - (e.l2 + e.l3 - sh.l4[t]) : 0.0;
+    }
+    // multipliers of a direction (complementarity rows with targets rc)
+    __device__ __forceinline__ void ddirs(const St& e, double rc1, double rc2, double rc3, double dw, double ds,
+                                          double dd, double& dl1, double& dl2, double& dl3) const {
+        dl1 = hw() ? (-rc1 - e.l1 * dw) * e.iw : 0.0;
+        dl2 = hs() ? (-rc2 - e.l2 * (ds - dd)) * e.iz2 : 0.0;
+        dl3 = hs() ? (-rc3 - e.l3 * (ds + dd)) * e.iz3 : 0.0;
+    }
+    __device__ __forceinline__ double alpha(int t, double m) const { return m * sh.iden[t] * irsig; }
+    __device__ __forceinline__ double eps(int t, const St& e) const { return ht() ? sh.sr[t] * e.bma * e.P : 0.0; }
+
+    // ---- reductions ----
+    // wave total of v into this wave's partial slot j (every lane of the wave must call)
+    __device__ __forceinline__ void slot(int j, double v) const {
+        v = wave_sum(v);
+        if ((threadIdx.x & (WAVE - 1)) == 0) sh.red[threadIdx.x / WAVE][j] = v;
+    }
+    // block totals of slots 0..n-1 -> sh.tot
+    __device__ __forceinline__ void finish(int n) const {
+        __syncthreads();
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            double s = sh.red[0][j];
+            for (int q = 1; q < nw; ++q) s += sh.red[q][j];
+            sh.tot[j] = s;
+        }
+        __syncthreads();
+    }
+    // block sum of s and block max of mx (one barrier)
+    __device__ __forceinline__ void sum_max(double& s, double& mx) {
+        s = wave_sum(s);
+        mx = wave_max(mx);
+        const int wv = threadIdx.x / WAVE;
+        if ((threadIdx.x & (WAVE - 1)) == 0) { sh.sc[sbuf][wv][0] = s; sh.sc[sbuf][wv][1] = mx; }
+        __syncthreads();
+        double S = sh.sc[sbuf][0][0], MX = sh.sc[sbuf][0][1];
+        for (int q = 1; q < nw; ++q) { S += sh.sc[sbuf][q][0]; MX = fmax(MX, sh.sc[sbuf][q][1]); }
+        s = S;
+        mx = MX;
+        sbuf ^= 1;
+    }
+};
+
+// (1) period sums R.w, 1'w, 1's -> den, iden, rp, rg4, rc4, iz4, rw (period owners)
+template <int HM, int FL>
+__device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
+    auto& sh = W.sh;
+    for (int t = 0; t < W.H; ++t) {
+        double mw = 0.0, w = 0.0, s = 0.0;
+        if (W.act) {
+            w = W.at(A_W, t);
+            mw = W.at(A_M, t) * w;
+            s = W.at(A_S, t);
+        }
+        W.slot(3 * t, mw);
+        W.slot(3 * t + 1, w);
+        W.slot(3 * t + 2, s);
+    }
+    W.finish(3 * W.H);
+    if (threadIdx.x < HM) {
+        const int t = threadIdx.x;
+        const bool on = t < W.H;
+        const double mw = on ? sh.tot[3 * t] : 0.0, sw = on ? sh.tot[3 * t + 1] : 0.0, ss = on ? sh.tot[3 * t + 2] : 0.0;
+        sh.rw[t] = sw + mw;   // sum_i exp(yhat) w = sum w + sum expm1(yhat) w
+        sh.den[t] = 1.0 + mw;
+        sh.iden[t] = 1.0 / (1.0 + mw);
+        sh.rp[t] = on ? sw - 1.0 : 0.0;
+        sh.rg4[t] = (W.ht() && on) ? W.tau - ss - sh.z4[t] : 0.0;
+        sh.rc4[t] = (W.ht() && on) ? sh.z4[t] * sh.l4[t] : 0.0;
+        sh.iz4[t] = 1.0 / sh.z4[t];
+        if (t == 0) sh.flag = 0;
+    }
+    __syncthreads();
+}
+
+// (2) dual residual and complementarity sums, per-asset LDL^T of Q (LR, IDD), targets rc (RC*),
+// sum_i P per period -> rho, sr (owners). Returns mu (unscaled block sum) and rd (block max).
+template <int HM, int FL>
+__device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& rd) {
+    auto& sh = W.sh;
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    mu_l = 0.0;
+    rd = 0.0;
+    bool ok = true;
+    St cur{};
+    double W1c = 0.0, Ec = 0.0, pi = 0.0, lr = 0.0;
+    if (W.act) {
+        cur = W.st(0, W.wpi);
+        W1c = cur.l1 * cur.iw;
+        Ec = hs ? 4.0 * (cur.l2 * cur.iz2) * (cur.l3 * cur.iz3) * cur.P : 0.0;
+        pi = W1c + Ec;
+    }
+    for (int t = 0; t < H; ++t) {
+        double P = 0.0;
+        if (W.act) {
+            const bool nx = t + 1 < H;
+            St nxt = cur;
+            double W1n = 0.0, En = 0.0;
+            if (nx) {
+                nxt = W.st(t + 1, cur.w);
+                W1n = nxt.l1 * nxt.iw;
+                En = hs ? 4.0 * (nxt.l2 * nxt.iz2) * (nxt.l3 * nxt.iz3) * nxt.P : 0.0;
+            }
+            double rdw, rds;
+            W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
+            const double r1 = hw ? cur.w * cur.l1 : 0.0;
+            const double r2 = hs ? (cur.s - cur.d) * cur.l2 : 0.0;
+            const double r3 = hs ? (cur.s + cur.d) * cur.l3 : 0.0;
+            mu_l += r1 + r2 + r3;
+            rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
+            P = cur.P;
+            W.at(A_RC1, t) = r1;
+            W.at(A_RC2, t) = r2;
+            W.at(A_RC3, t) = r3;
+            // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
+            const double Dd = pi + (nx ? En : 0.0);
+            ok = ok && (Dd > 0.0) && (Dd < 1e300);
+            const double iDd = rcp(Dd);
+            W.at(A_IDD, t) = iDd;
+            W.at(A_LR, t) = lr;
+            if (nx) {
+                lr = En * iDd;
+                pi = W1n + lr * pi;
+            }
+            cur = nxt;
+        }
+        W.slot(t, P);
+    }
+    W.finish(H);
+    if (threadIdx.x < HM) {
+        const int t = threadIdx.x;
+        const double st = t < H ? sh.tot[t] : 0.0;
+        const double ga = (ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
+        sh.rho[t] = (ht && t < H) ? ga / (1.0 + ga * st) : 0.0;
+        sh.sr[t] = sqrt(sh.rho[t]);
+    }
+    if (!ok) sh.flag = 1;
+    W.sum_max(mu_l, rd);   // (its barrier publishes rho, sr and flag)
+}
+
+// W (t < tw) of the current iterate to the output, and the per-period ||w_t - w_{t-1}||_1 and R.w
+// of this iterate (its objective is evaluated after the loop)
+template <int HM, int FL>
+__device__ __forceinline__ void ph_record(Win<HM, FL>& W, double* wout, int tw) {
+    auto& sh = W.sh;
+    double wprev = W.wpi;
+    for (int t = 0; t < W.H; ++t) {
+        double v = 0.0;
+        if (W.act) {
+            const double w = W.at(A_W, t);
+            if (t < tw) wout[t * W.N + W.i] = w;
+            v = fabs(w - wprev);
+            wprev = w;
+        }
+        W.slot(t, v);
+    }
+    W.finish(W.H);
+    if (threadIdx.x < HM) {
+        sh.best_rw[threadIdx.x] = sh.rw[threadIdx.x];
+        sh.best_l1[threadIdx.x] = (int)threadIdx.x < W.H ? sh.tot[threadIdx.x] : 0.0;
+    }
+}
+
+// (3) Schur matrix: generators (slab) and the direct (v_t, v_t) sums, MFMA tiles of Lgen^T Rgen
+template <int HM, int FL>
+__device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
+    auto& sh = W.sh;
+    const int H = W.H, K3 = 3 * H, N4 = (W.N + 3) & ~3;
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    // diagonal of Q^{-1} (dq_t = 1/Dd_t + Lr_{t+1}^2 dq_{t+1}) into X; pi_H for the centring
+    int e = 0;
+    if (W.act) {
+        double dqn = 0.0, lrn = 0.0;
+        for (int t = H - 1; t >= 0; --t) {
+            const double dq = W.at(A_IDD, t) + lrn * lrn * dqn;
+            W.at(A_X, t) = dq;
+            dqn = dq;
+            lrn = W.at(A_LR, t);
+        }
+        double pi = 1.0;
+        for (int t = 1; t < H; ++t) pi *= fmax(W.at(A_LR, t), LR_FLOOR);
+        frexp(pi, &e);
+    }
+    const double cen = ldexp(1.0, -(e / 2));
+    double wprev = W.wpi, pi = 1.0, gp = 0.0, bp = 0.0, dqp = 0.0;
+    for (int t = 0; t < H; ++t) {
+        double vv = 0.0;
+        if (W.act) {
+            const St s = W.st(t, wprev);
+            wprev = s.w;
+            const double lr = W.at(A_LR, t), dq = W.at(A_X, t);
+            if (t) pi *= fmax(lr, LR_FLOOR);
+            const double al = W.alpha(t, s.m), ep = W.eps(t, s);
+            const double pt = pi * cen, gt = 1.0 / pt, bt = dq * pt;
+            W.lg(3 * t)[W.i] = ep * (gt - gp);
+            W.lg(3 * t + 1)[W.i] = al * gt;
+            W.lg(3 * t + 2)[W.i] = gt;
+            W.rg(3 * t)[W.i] = ep * (bt - bp);
+            W.rg(3 * t + 1)[W.i] = al * bt;
+            W.rg(3 * t + 2)[W.i] = bt;
+            // (v_t, v_t) = ep^2 (Qi[t][t] - 2 Qi[t-1][t] + Qi[t-1][t-1]), Qi[t-1][t] = Lr_t dq_t
+            vv = t ? ep * ep * (dq - 2.0 * lr * dq + dqp) : ep * ep * dq;
+            gp = gt;
+            bp = bt;
+            dqp = dq;
+        } else if (W.i < N4) {
+            // padding assets of the last K group of the MFMA loop contribute zeros
+            for (int ty = 0; ty < 3; ++ty) { W.lg(3 * t + ty)[W.i] = 0.0; W.rg(3 * t + ty)[W.i] = 0.0; }
+        }
+        W.slot(t, vv);
+    }
+    W.finish(H);   // (its barriers also publish the generators to the workgroup)
+    if ((int)threadIdx.x < H) sh.G[(3 * threadIdx.x) * LDG + 3 * threadIdx.x] = sh.tot[threadIdx.x];
+    // tiles (I, J), I <= J, of the 16-blocks in use, one wave per tile
+    const int NB = (K3 + 15) / 16, ntile = NB * (NB + 1) / 2;
+    for (int q = wv; q < ntile; q += W.nw) {
+        int I = 0, J = 0, rem = q;
+        for (int bi = 0; bi < NB; ++bi) {
+            const int n = NB - bi;
+            if (rem < n) { I = bi; J = bi + rem; break; }
+            rem -= n;
+        }
+        const double* pa = W.lg(16 * I + (lane & 15)) + (lane >> 4);
+        const double* pb = W.rg(16 * J + (lane & 15)) + (lane >> 4);
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k0 = 0; k0 < N4; k0 += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k0], pb[k0], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int j = 16 * I + (lane >> 4) + 4 * r, l = 16 * J + (lane & 15);
+            if (j < K3 && l < K3) {
+                const int tj = j / 3, tyj = j - 3 * tj, tl = l / 3, tyl = l - 3 * tl;
+                const bool use = tj < tl || (tj == tl && tyj <= tyl && !(tyj == 0 && tyl == 0));
+                if (use) sh.G[l * LDG + j] = acc[r];
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// Wave 0: G + I' = L D L^T in LDS (lane r owns row r; unused rows become identity). Right-looking:
+// step j scales column j and updates the trailing rows, one LDS read-modify-write per entry.
+template <int HM>
+__device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht) {
+    if (threadIdx.x < WAVE) {
+        const int K3 = 3 * H;
+        const int r = threadIdx.x;
+        const int ty = r % 3;
+        const bool rused = r < K3 && (ty != 0 || ht);
+        // assemble row r (lower triangle) with I' and identity rows
+        if (r < K3) {
+            for (int k = 0; k <= r; ++k) {
+                const int tyk = k % 3;
+                const bool kused = tyk != 0 || ht;
+                double v = (rused && kused) ? sh.G[r * LDG + k] : 0.0;
+                if (k == r) v += (ty != 2 || !rused) ? 1.0 : 0.0;
+                sh.G[r * LDG + k] = v;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        bool bad = false;
+        for (int j = 0; j < K3; ++j) {
+            const double d = sh.G[j * LDG + j];
+            bad = bad || !(d > 0.0) || !(d < 1e300);
+            const double id = rcp(fmax(d, 1e-300));
+            if (r == j) sh.gid[j] = id;
+            const bool below = r > j && r < K3;
+            const double l = below ? sh.G[r * LDG + j] * id : 0.0;
+            __builtin_amdgcn_wave_barrier();
+            if (below)
+                for (int k = j + 1; k <= r; ++k) sh.G[r * LDG + k] = fma(-l, sh.G[k * LDG + j], sh.G[r * LDG + k]);
+            __builtin_amdgcn_wave_barrier();
+            if (below) sh.G[r * LDG + j] = l;
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (bad && r == 0) sh.flag = 1;
+    }
+    __syncthreads();
+}
+
+// Wave 0: q = G^{-1} rhs, rhs[3t + type] from sh.tot (type-major slots tot[type * H + t]),
+// budget rows minus lb6 -> sh.q
+template <int HM>
+__device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H) {
+    if (threadIdx.x < WAVE) {
+        const int K3 = 3 * H;
+        const int lane = threadIdx.x;
+        double x = 0.0;
+        if (lane < K3) {
+            const int t = lane / 3, ty = lane - 3 * t;
+            x = sh.tot[ty * H + t];
+            if (ty == 2) x -= sh.lb6[t];
+        }
+        // forward: L y = rhs (lane r reads row r of L), then D^{-1}
+        const int lr = lane < K3 ? lane : 0;
+        for (int j = 0; j + 1 < K3; ++j) {
+            const double yj = bcast(x, j);
+            if (lane > j) x = fma(-sh.G[lr * LDG + j], yj, x);
+        }
+        x *= sh.gid[lr];
+        // backward: L^T q = y (lane r reads column r of L)
+        for (int j = K3 - 1; j > 0; --j) {
+            const double qj = bcast(x, j);
+            if (lane < j) x = fma(-sh.G[j * LDG + lr], qj, x);
+        }
+        if (lane < K3) sh.q[lane] = x;
+    }
+    __syncthreads();
+}
+
+// Newton solve for rhs rows (first: -rdw, -rds with the complementarity targets rc; refinement:
+// the residual arrays R0 / R1, no targets), oracle/kmpc_oracle.c:lsolve. The solution is assigned
+// (first) or added to DW, DS and sh.dnu.
+template <int HM, int FL>
+__device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
+    auto& sh = W.sh;
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    // ---- A: right-hand sides (BW, BS) and px = sum_i P bs ----
+    {
+        St cur{};
+        double rc2c = 0.0, rc3c = 0.0;
+        if (W.act) {
+            cur = W.st(0, W.wpi);
+            if (first && hs) { rc2c = W.at(A_RC2, 0); rc3c = W.at(A_RC3, 0); }
+        }
+        for (int t = 0; t < H; ++t) {
+            double px = 0.0;
+            if (W.act) {
+                const bool nx = t + 1 < H;
+                St nxt = cur;
+                double rc2n = 0.0, rc3n = 0.0;
+                if (nx) {
+                    nxt = W.st(t + 1, cur.w);
+                    if (first && hs) { rc2n = W.at(A_RC2, t + 1); rc3n = W.at(A_RC3, t + 1); }
+                }
+                double b0, b1, p1 = 0.0, p2 = 0.0, p3 = 0.0, pn = 0.0;
+                if (first) {
+                    double rdw, rds;
+                    W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
+                    b0 = -rdw;
+                    b1 = -rds;
+                    p1 = hw ? -W.at(A_RC1, t) * cur.iw : 0.0;
+                    if (hs) {
+                        p2 = -rc2c * cur.iz2;
+                        p3 = -rc3c * cur.iz3;
+                        if (nx) pn = -rc3n * nxt.iz3 + rc2n * nxt.iz2;
+                    }
+                } else {
+                    b0 = W.at(A_R0, t);
+                    b1 = W.at(A_R1, t);
+                }
+                const double bw = b0 + p1 + (p3 - p2) - pn;
+                const double bs = hs ? b1 + p2 + p3 - (ht ? sh.lb5[t] * sh.iz4[t] : 0.0) : 0.0;
+                W.at(A_BW, t) = bw;
+                W.at(A_BS, t) = bs;
+                px = cur.P * bs;
+                cur = nxt;
+                rc2c = rc2n;
+                rc3c = rc3n;
+            }
+            W.slot(t, px);
+        }
+        W.finish(H);
+        if (threadIdx.x < HM) sh.px[threadIdx.x] = (int)threadIdx.x < H ? sh.tot[threadIdx.x] : 0.0;
+        __syncthreads();
+    }
+    // ---- B: s elimination, x = Q^{-1} rhs_w (X), Schur rhs Z^T x, q = G^{-1} (...) ----
+    {
+        if (W.act) {
+            // rhs_w -= g_t - g_{t+1}, g = bma P (bs - rho px); forward sweep y_t = x_t + Lr_t y_{t-1} (Y)
+            double y = 0.0;
+            St cur = W.st(0, W.wpi);
+            double gc = hs ? cur.bma * cur.P * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
+            for (int t = 0; t < H; ++t) {
+                double gn = 0.0;
+                St nxt = cur;
+                if (t + 1 < H) {
+                    nxt = W.st(t + 1, cur.w);
+                    gn = hs ? nxt.bma * nxt.P * (W.at(A_BS, t + 1) - sh.rho[t + 1] * sh.px[t + 1]) : 0.0;
+                }
+                const double x = W.at(A_BW, t) - gc + gn;
+                y = x + W.at(A_LR, t) * y;
+                W.at(A_Y, t) = y;
+                cur = nxt;
+                gc = gn;
+            }
+        }
+        // backward sweep x_t = y_t / Dd_t + Lr_{t+1} x_{t+1} (X), with the Z^T x slots: at step t,
+        // v-slot t+1 = eps_{t+1} (x_{t+1} - x_t), a-slot t = alpha_t x_t, 1-slot t = x_t
+        double xn = 0.0, lrn = 0.0, epn = 0.0;
+        for (int t = H - 1; t >= 0; --t) {
+            double x = 0.0, va = 0.0, vv1 = 0.0, ep = 0.0;
+            if (W.act) {
+                x = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * xn;
+                W.at(A_X, t) = x;
+                const St s = W.st(t, W.wprev(t));
+                ep = W.eps(t, s);
+                va = W.alpha(t, s.m) * x;
+                vv1 = (t + 1 < H) ? epn * (xn - x) : 0.0;
+                lrn = W.at(A_LR, t);
+            }
+            if (t + 1 < H) W.slot(t + 1, vv1);
+            W.slot(H + t, va);
+            W.slot(2 * H + t, x);
+            if (t == 0) W.slot(0, W.act ? ep * x : 0.0);
+            xn = x;
+            epn = ep;
+        }
+        W.finish(3 * H);
+        schur_solve(sh, H);
+    }
+    // ---- C: dw = x - Q^{-1} (Z q) (DW), bs -= bma dd (BS), px = sum_i P bs ----
+    {
+        if (W.act) {
+            // Z q per period: alpha_t q_a + q_1 + eps_t q_v(t) - eps_{t+1} q_v(t+1); forward sweep (Y)
+            double y = 0.0;
+            St cur = W.st(0, W.wpi);
+            double epc = W.eps(0, cur);
+            for (int t = 0; t < H; ++t) {
+                double epn = 0.0;
+                St nxt = cur;
+                if (t + 1 < H) {
+                    nxt = W.st(t + 1, cur.w);
+                    epn = W.eps(t + 1, nxt);
+                }
+                const double zq = W.alpha(t, cur.m) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
+                                  ((t + 1 < H) ? epn * sh.q[3 * t + 3] : 0.0);
+                y = zq + W.at(A_LR, t) * y;
+                W.at(A_Y, t) = y;
+                cur = nxt;
+                epc = epn;
+            }
+        }
+        // backward sweep; dw_t = x_t - (Q^{-1} Z q)_t; at step t: bs_{t+1} -= bma_{t+1} (dw_{t+1} - dw_t)
+        double tn = 0.0, lrn = 0.0, dwn = 0.0, bman = 0.0, Pn = 0.0;
+        for (int t = H - 1; t >= 0; --t) {
+            double pxn = 0.0, px0 = 0.0;
+            if (W.act) {
+                const double tq = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * tn;
+                tn = tq;
+                lrn = W.at(A_LR, t);
+                const double dw = W.at(A_X, t) - tq;
+                if (first) W.at(A_DW, t) = dw; else W.at(A_DW, t) += dw;
+                const St s = W.st(t, W.wprev(t));
+                if (hs && t + 1 < H) {
+                    const double bs = W.at(A_BS, t + 1) - bman * (dwn - dw);
+                    W.at(A_BS, t + 1) = bs;
+                    pxn = Pn * bs;
+                }
+                if (hs && t == 0) {
+                    const double bs = W.at(A_BS, 0) - s.bma * dw;
+                    W.at(A_BS, 0) = bs;
+                    px0 = s.P * bs;
+                }
+                dwn = dw;
+                bman = s.bma;
+                Pn = s.P;
+            }
+            if (t + 1 < H) W.slot(t + 1, pxn);
+            if (t == 0) W.slot(0, px0);
+        }
+        W.finish(H);
+    }
+    // ---- D: ds = P (bs - rho px) (DS); budget multipliers ----
+    {
+        if (W.act) {
+            for (int t = 0; t < H; ++t) {
+                double ds = 0.0;
+                if (hs) {
+                    const St s = W.st(t, W.wprev(t));
+                    ds = s.P * (W.at(A_BS, t) - sh.rho[t] * sh.tot[t]);
+                }
+                if (first) W.at(A_DS, t) = ds; else W.at(A_DS, t) += ds;
+            }
+        }
+        if (threadIdx.x < HM) {
+            const int t = threadIdx.x;
+            const double dn = t < H ? sh.q[3 * t + 2] : 0.0;
+            sh.dnu[t] = first ? dn : sh.dnu[t] + dn;
+        }
+        __syncthreads();
+    }
+}
+
+// Newton direction for the current rc targets, adaptive refinement (ipm_kernel newton).
+// On exit: DW, DS, sh.dnu, sh.dz4, sh.dl4.
+template <int HM, int FL>
+__device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine) {
+    auto& sh = W.sh;
+    const bool hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    if (threadIdx.x < HM) {
+        const int t = threadIdx.x;
+        sh.b5[t] = (ht && t < H) ? -sh.rc4[t] - sh.l4[t] * sh.rg4[t] : 0.0;
+        sh.b6[t] = (t < H) ? -sh.rp[t] : 0.0;
+        sh.lb5[t] = sh.b5[t];
+        sh.lb6[t] = sh.b6[t];
+    }
+    __syncthreads();
+    double bn = 0.0;
+    if (n_refine > 0) {   // ||b||_inf of the unreduced system
+        if (W.act) {
+            St cur = W.st(0, W.wpi);
+            for (int t = 0; t < H; ++t) {
+                const bool nx = t + 1 < H;
+                const St nxt = nx ? W.st(t + 1, cur.w) : cur;
+                double rdw, rds;
+                W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
+                bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
+                                   fmax(fabs(W.at(A_RC1, t)), fmax(fabs(W.at(A_RC2, t)), fabs(W.at(A_RC3, t))))));
+                cur = nxt;
+            }
+        }
+        if (threadIdx.x == 0)
+            for (int t = 0; t < H; ++t) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
+        double z = 0.0;
+        W.sum_max(z, bn);
+    }
+    for (int r = 0;; ++r) {
+        ph_lsolve(W, r == 0);
+        if (r >= n_refine) break;
+        // residual of rows (1), (2), (7) of the direction; rows (3)-(6) hold by construction
+        for (int t = 0; t < H; ++t) {
+            double va = 0.0, vs = 0.0, vw = 0.0;
+            if (W.act) {
+                vw = W.at(A_DW, t);
+                va = W.alpha(t, W.at(A_M, t)) * vw;
+                vs = W.at(A_DS, t);
+            }
+            W.slot(t, va);
+            W.slot(H + t, vs);
+            W.slot(2 * H + t, vw);
+        }
+        W.finish(3 * H);
+        if (threadIdx.x < HM) {
+            const int t = threadIdx.x;
+            const bool on = t < H;
+            sh.adw[t] = on ? sh.tot[t] : 0.0;
+            sh.sds[t] = on ? sh.tot[H + t] : 0.0;
+            sh.sdw[t] = on ? sh.tot[2 * H + t] : 0.0;
+        }
+        __syncthreads();
+        double rn = 0.0;
+        if (W.act) {
+            double nl2 = 0.0, nl3 = 0.0, l2n = 0.0, l3n = 0.0;   // dl2 / dl3 / l2 / l3 of period t + 1
+            for (int t = H - 1; t >= 0; --t) {
+                const St e = W.st(t, W.wprev(t));
+                const double dw = W.at(A_DW, t), ds = W.at(A_DS, t);
+                const double dd = dw - (t ? W.at(A_DW, t - 1) : 0.0);
+                double dl1, dl2, dl3;
+                W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+                double rdw, rds;
+                W.dres(t, e, l2n, l3n, rdw, rds);
+                const double dl4 = ht ? (sh.b5[t] + sh.l4[t] * sh.sds[t]) * sh.iz4[t] : 0.0;
+                const double r0 = -rdw - (W.alpha(t, e.m) * sh.adw[t] - (dl1 + (dl3 - dl2) - (nl3 - nl2)) + sh.dnu[t]);
+                const double r1 = hs ? -rds + (dl2 + dl3 - dl4) : 0.0;
+                W.at(A_R0, t) = r0;
+                W.at(A_R1, t) = r1;
+                rn = fmax(rn, fmax(fabs(r0), fabs(r1)));
+                nl2 = dl2;
+                nl3 = dl3;
+                l2n = e.l2;
+                l3n = e.l3;
+            }
+        }
+        if (threadIdx.x == 0)
+            for (int t = 0; t < H; ++t) rn = fmax(rn, fabs(sh.b6[t] - sh.sdw[t]));
+        {
+            double z = 0.0;
+            W.sum_max(z, rn);
+        }
+        if (rn <= REFINE_RTOL * bn) break;
+        if (threadIdx.x < HM) {
+            const int t = threadIdx.x;
+            sh.lb5[t] = 0.0;                                   // row (6) residual is identically 0
+            sh.lb6[t] = (t < H) ? sh.b6[t] - sh.sdw[t] : 0.0;
+        }
+        __syncthreads();
+    }
+    // dz4 / dl4 of the final direction
+    for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.at(A_DS, t) : 0.0);
+    W.finish(H);
+    if (threadIdx.x < HM) {
+        const int t = threadIdx.x;
+        const bool on = ht && t < H;
+        const double st = t < H ? sh.tot[t] : 0.0;
+        sh.dz4[t] = on ? -st + sh.rg4[t] : 0.0;
+        sh.dl4[t] = on ? (sh.b5[t] + sh.l4[t] * st) * sh.iz4[t] : 0.0;
+    }
+    __syncthreads();
+}
+
+// Largest step for the current direction (before the fraction-to-boundary)
+template <int HM, int FL>
+__device__ __forceinline__ double ph_step(Win<HM, FL>& W) {
+    auto& sh = W.sh;
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    double a = 1e300, wprev = W.wpi, dwp = 0.0;
+    for (int t = 0; t < H; ++t) {
+        double mdw = 0.0;
+        if (W.act) {
+            const St e = W.st(t, wprev);
+            wprev = e.w;
+            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            dwp = dw;
+            double dl1, dl2, dl3;
+            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+            if (hw) { a = to_bound(e.w, dw, a); a = to_bound(e.l1, dl1, a); }
+            if (hs) {
+                a = to_bound(e.s - e.d, ds - dd, a);
+                a = to_bound(e.s + e.d, ds + dd, a);
+                a = to_bound(e.l2, dl2, a);
+                a = to_bound(e.l3, dl3, a);
+            }
+            mdw = e.m * dw;
+        }
+        W.slot(t, mdw);
+    }
+    {
+        double z = 0.0, na = -a;
+        W.sum_max(z, na);
+        a = -na;
+    }
+    W.finish(H);
+    for (int t = 0; t < H; ++t) {
+        a = to_bound(sh.den[t], sh.tot[t], a);
+        if (ht) { a = to_bound(sh.z4[t], sh.dz4[t], a); a = to_bound(sh.l4[t], sh.dl4[t], a); }
+    }
+    return a;
+}
+
+template <int HM, int FL>
+__device__ __forceinline__ double ph_comp(Win<HM, FL>& W, double a) {
+    auto& sh = W.sh;
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    double acc = 0.0;
+    if (W.act) {
+        double wprev = W.wpi, dwp = 0.0;
+        for (int t = 0; t < H; ++t) {
+            const St e = W.st(t, wprev);
+            wprev = e.w;
+            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            dwp = dw;
+            double dl1, dl2, dl3;
+            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+            if (hw) acc += (e.w + a * dw) * (e.l1 + a * dl1);
+            if (hs) {
+                acc += (e.s - e.d + a * (ds - dd)) * (e.l2 + a * dl2);
+                acc += (e.s + e.d + a * (ds + dd)) * (e.l3 + a * dl3);
+            }
+        }
+    }
+    double z = 0.0;
+    W.sum_max(acc, z);
+    if (ht)
+        for (int t = 0; t < H; ++t) acc += (sh.z4[t] + a * sh.dz4[t]) * (sh.l4[t] + a * sh.dl4[t]);
+    return acc;
+}
+
+// corrector targets: rc += dz_aff dl_aff - sigma mu (rc4 by its owner)
+template <int HM, int FL>
+__device__ __forceinline__ void ph_corr(Win<HM, FL>& W, double smu) {
+    auto& sh = W.sh;
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int H = W.H;
+    if (W.act) {
+        double wprev = W.wpi, dwp = 0.0;
+        for (int t = 0; t < H; ++t) {
+            const St e = W.st(t, wprev);
+            wprev = e.w;
+            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            dwp = dw;
+            const double rc1 = W.at(A_RC1, t), rc2 = W.at(A_RC2, t), rc3 = W.at(A_RC3, t);
+            double dl1, dl2, dl3;
+            W.ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
+            if (hw) W.at(A_RC1, t) = rc1 + (dw * dl1 - smu);
+            if (hs) {
+                W.at(A_RC2, t) = rc2 + ((ds - dd) * dl2 - smu);
+                W.at(A_RC3, t) = rc3 + ((ds + dd) * dl3 - smu);
+            }
+        }
+    }
+    if (threadIdx.x < HM && ht && (int)threadIdx.x < H) {
+        const int t = threadIdx.x;
+        sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
+    }
+    __syncthreads();
+}
+
+// iterate update (the multiplier directions need the old state: w_{t-1} is carried)
+template <int HM, int FL>
+__device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
+    auto& sh = W.sh;
+    const int H = W.H;
+    if (W.act) {
+        double wprev = W.wpi, dwp = 0.0;
+        for (int t = 0; t < H; ++t) {
+            const St e = W.st(t, wprev);
+            wprev = e.w;
+            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            dwp = dw;
+            double dl1, dl2, dl3;
+            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+            W.at(A_L1, t) = e.l1 + step * dl1;
+            W.at(A_L2, t) = e.l2 + step * dl2;
+            W.at(A_L3, t) = e.l3 + step * dl3;
+            W.at(A_W, t) = e.w + step * dw;
+            W.at(A_S, t) = e.s + step * ds;
+        }
+    }
+    __syncthreads();   // every ratio test has read z4 / l4 before their owners update them
+    if (threadIdx.x < HM && (int)threadIdx.x < H) {
+        const int t = threadIdx.x;
+        sh.z4[t] += step * sh.dz4[t];
+        sh.l4[t] += step * sh.dl4[t];
+        sh.nu[t] += step * sh.dnu[t];
+    }
+    __syncthreads();
+}
+
+template <int HM, int FL>
+__device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw, double inv_ncon, double& best,
+                                        double& min_pr, int b) {
+    auto& sh = W.sh;
+    const SolveArgs& a = W.a;
+    const int H = W.H;
+    int it;
+    for (it = 0; it < a.max_iter; ++it) {
+        ph_sums(W);
+        double mu_l, rd;
+        ph_factor(W, mu_l, rd);
+        double mu = mu_l, pr = 0.0;
+        bool domain_ok = true;
+        for (int t = 0; t < H; ++t) {
+            mu += sh.rc4[t];
+            pr = fmax(pr, fmax(fabs(sh.rp[t]), fabs(sh.rg4[t])));
+            domain_ok = domain_ok && sh.den[t] > 0.0;
+        }
+        mu *= inv_ncon;
+        const double merit = fmax(mu, fmax(rd, pr));
+        min_pr = fmin(min_pr, pr);
+        if (a.trace && b == 0 && threadIdx.x == 0) {
+            a.trace[4 * it + 0] = mu; a.trace[4 * it + 1] = rd; a.trace[4 * it + 2] = pr;
+        }
+        if (!domain_ok || !isfinite(merit)) break;
+        if (merit < best) {
+            best = merit;
+            ph_record(W, wout, tw);
+        } else if (best < 1e-6 && merit > 1e4 * best) {
+            break;   // numerical breakdown after convergence: keep the best iterate
+        }
+        if (mu < a.tol && rd < 10.0 * a.tol && pr < 10.0 * a.tol) break;
+        if (sh.flag) break;   // Q not positive definite
+        ph_gram(W);
+        schur_factor(sh, H, W.ht());
+        if (sh.flag) break;
+        double step = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            ph_newton(W, (pass == 0 || mu > REFINE_MU) ? 0 : a.n_refine);
+            const double amax = ph_step(W);
+            if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
+            const double ap = fmin(1.0, amax);
+            double sg = ph_comp(W, ap) * inv_ncon / mu;
+            sg = sg * sg * sg;
+            ph_corr(W, sg * mu);
+        }
+        if (a.trace && b == 0 && threadIdx.x == 0) a.trace[4 * it + 3] = step;
+        ph_update(W, step);
+    }
+    return it;
+}
+
+template <int HM, int MAXT, int FL>
+__global__ void __launch_bounds__(MAXT) ipm_big(BigArgs A) {
+    static_assert(3 * HM <= KP - 1, "Schur system must fit one wave");
+    __shared__ BigShared<HM> sh;
+    const SolveArgs& a = A.s;
+    Win<HM, FL> W{a, sh, A.ws + (size_t)blockIdx.x * A.slab, a.N, a.H, A.NP, (int)(blockDim.x / WAVE),
+                  (int)threadIdx.x, (int)threadIdx.x < a.N};
+    W.sbuf = 0;
+    W.cs.set_case(!a.allow_short, (a.c > 0.0) || (a.tau > 0.0), a.tau > 0.0);
+    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
+    const int N = a.N, H = a.H, i = threadIdx.x;
+
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        const double* wp = a.wp + (size_t)b * N;
+        const float* yh = a.yhat + (size_t)b * H * N;
+        double* wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
+        const int tw = a.return_full ? H : 1;
+        W.wpi = W.act ? wp[i] : 0.0;
+
+        // ---- inputs: m = expm1(yhat) (slab), objective scale, finiteness ----
+        double mx = 0.0, nf = 0.0;
+        if (W.act) {
+            if (!isfinite(W.wpi)) nf = 1.0;
+            for (int t = 0; t < H; ++t) {
+                const double y = (double)yh[t * N + i];
+                if (!isfinite(y)) nf = 1.0;
+                const double m = expm1(y);
+                W.at(A_M, t) = m;
+                mx = fmax(mx, fabs(m));
+            }
+        }
+        {
+            double z = 0.0;
+            W.sum_max(z, mx);
+            z = 0.0;
+            W.sum_max(z, nf);
+        }
+        double sig = fmax(mx, a.c);
+        if (!(sig > 0.0)) sig = 1.0;
+        W.isig = 1.0 / sig;
+        W.irsig = 1.0 / sqrt(sig);
+        W.cs_c = a.c / sig;
+        W.tau = a.tau;
+
+        int status = KMPC_STATUS_SOLVER_ERROR, it = 0;
+        double best_obj = __builtin_nan("");
+
+        if (nf == 0.0 && isfinite(a.c) && isfinite(a.tau)) {
+            if (a.allow_short && !hs) {
+                // no bounds and no turnover terms: unbounded unless every period is flat
+                for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.at(A_M, t) : 0.0);
+                W.finish(H);
+                double spread = 0.0, swp = W.wpi;
+                if (W.act)
+                    for (int t = 0; t < H; ++t) spread = fmax(spread, fabs(W.at(A_M, t) - sh.tot[t] / N));
+                W.sum_max(swp, spread);
+                if (spread == 0.0) {
+                    const double w = swp != 0.0 ? W.wpi / swp : 1.0 / N;
+                    for (int t = 0; t < H; ++t) {
+                        if (W.act && t < tw) wout[t * N + i] = w;
+                        W.slot(t, W.act ? (1.0 + W.at(A_M, t)) * w : 0.0);
+                    }
+                    W.finish(H);
+                    double f = 0.0;
+                    for (int t = 0; t < H; ++t) f += log(sh.tot[t]);
+                    best_obj = f;
+                    status = KMPC_STATUS_OPTIMAL;
+                } else {
+                    status = KMPC_STATUS_UNBOUNDED;
+                }
+            } else {
+                // ---- initial point (as ipm_kernel / the oracle) ----
+                const double b0 = hw ? fmax(W.wpi, 0.0) : W.wpi;
+                const double w0 = 0.5 * b0 + 0.5 / N;
+                for (int t = 0; t < H; ++t) {
+                    double s = 0.0;
+                    if (W.act) {
+                        const double d = w0 - (t ? w0 : W.wpi);
+                        s = hs ? fabs(d) + 1.0 / N : 0.0;
+                        W.at(A_W, t) = w0;
+                        W.at(A_S, t) = s;
+                        W.at(A_L1, t) = hw ? 1.0 : 0.0;
+                        W.at(A_L2, t) = hs ? 1.0 : 0.0;
+                        W.at(A_L3, t) = hs ? 1.0 : 0.0;
+                    }
+                    W.slot(t, s);
+                }
+                W.finish(H);
+                if (threadIdx.x < HM) {
+                    const int t = threadIdx.x;
+                    sh.z4[t] = (ht && t < H) ? fmax(a.tau - sh.tot[t], 0.5 * a.tau) : 1.0;
+                    sh.l4[t] = (ht && t < H) ? 1.0 : 0.0;
+                    sh.nu[t] = 0.0;
+                }
+                __syncthreads();
+                const int ncon = (hw ? H * N : 0) + (hs ? 2 * H * N : 0) + (ht ? H : 0);
+                const double inv_ncon = 1.0 / (ncon > 0 ? ncon : 1);
+                double best = 1e300, min_pr = 1e300;
+                it = ipm_iterate(W, wout, tw, inv_ncon, best, min_pr, b);
+                __syncthreads();   // sh.best_* of the best iterate visible
+                if (best < 1e300) {
+                    double f = 0.0;
+                    for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) - a.c * sh.best_l1[t];
+                    best_obj = f;
+                }
+                if (best <= 1e-7) status = KMPC_STATUS_OPTIMAL;
+                else if (best <= 1e-4) status = KMPC_STATUS_OPTIMAL_INACCURATE;
+                else if (min_pr > 1e-6) status = KMPC_STATUS_INFEASIBLE;   // primal residual never closed
+                else status = KMPC_STATUS_SOLVER_ERROR;
+            }
+        }
+        __syncthreads();
+        // ---- outputs: W was written by ph_record; fallback (mpc.py:113-115) otherwise ----
+        const bool ok = status == KMPC_STATUS_OPTIMAL || status == KMPC_STATUS_OPTIMAL_INACCURATE;
+        if (!ok && W.act)
+            for (int t = 0; t < tw; ++t) wout[t * N + i] = W.wpi;
+        if (threadIdx.x == 0) {
+            a.obj[b] = ok ? best_obj : __builtin_nan("");
+            a.status[b] = status;
+            if (a.iters) a.iters[b] = it;
+        }
+        __syncthreads();
+    }
+}
+
+// workspace bytes of the large-window launch
+template <int HM>
+size_t ws_bytes(const SolveArgs& a) {
+    const int NP = WAVE * ((a.N + WAVE - 1) / WAVE);
+    const int slots = a.B < MAX_SLOTS ? a.B : MAX_SLOTS;
+    return sizeof(double) * slab_doubles(HM, NP) * (size_t)slots;
+}
+
+template <int HM, int MAXT>
+int launch_t(const BigArgs& A, int slots, hipStream_t stream, int fl) {
+    if (fl == 7) hipLaunchKernelGGL((ipm_big<HM, MAXT, 7>), dim3(slots), dim3(A.NP), 0, stream, A);
+    else hipLaunchKernelGGL((ipm_big<HM, MAXT, -1>), dim3(slots), dim3(A.NP), 0, stream, A);
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+template <int HM>
+int launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream) {
+    if (a.N > NWX * WAVE || a.H > HM) return KMPC_ERR_UNSUPPORTED;
+    if (!ws || ws_size < ws_bytes<HM>(a)) return KMPC_ERR_WORKSPACE;
+    BigArgs A;
+    A.s = a;
+    A.NP = WAVE * ((a.N + WAVE - 1) / WAVE);
+    A.slab = slab_doubles(HM, A.NP);
+    A.ws = (double*)ws;
+    const int slots = a.B < MAX_SLOTS ? a.B : MAX_SLOTS;
+    const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
+    if (A.NP <= 256) return launch_t<HM, 256>(A, slots, stream, fl);
+    if (A.NP <= 512) return launch_t<HM, 512>(A, slots, stream, fl);
+    return launch_t<HM, 1024>(A, slots, stream, fl);
+}
+
+}  // namespace big
+}  // namespace kmpc

@@ -49,6 +49,24 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     return d
 
 
+_WS = {}   # solve workspaces per (device, HIP stream): calls on different streams never share one
+
+
+def _solve_workspace(d: _lib.SolveDesc, device: torch.device) -> Tuple[int, int]:
+    """(pointer, bytes) of a workspace large enough for the solve described by d (the large-window
+    kernel keeps each window's interior-point state there; the register kernels need none)."""
+    L = _lib.load()
+    nbytes = int(L.kmpc_workspace_bytes(None, ctypes.byref(d)))
+    if nbytes == 0:
+        return 0, 0
+    key = (device.index, _lib.stream_handle(device) or 0)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws.data_ptr(), ws.numel()
+
+
 def solve_mpc_log_utility_batched(
     current_weights: torch.Tensor,
     predicted_log_returns: torch.Tensor,
@@ -87,8 +105,9 @@ def solve_mpc_log_utility_batched(
     d = _solve_desc(B, N, H, config, return_full)
     L = _lib.load()
     with torch.cuda.device(y.device):
+        ws, nws = _solve_workspace(d, y.device)
         rc = L.kmpc_solve(ctypes.byref(d), y.data_ptr(), wp.data_ptr(), W.data_ptr(),
-                          status.data_ptr(), value.data_ptr(), iters.data_ptr(), None, 0,
+                          status.data_ptr(), value.data_ptr(), iters.data_ptr(), ws or None, nws,
                           _lib.stream_handle(y.device))
     _lib.check(rc)
     if with_iters:

@@ -8,13 +8,15 @@ N, H, c, tau = [int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3]), float(sy
 rng = np.random.default_rng(0)
 wp = rng.dirichlet(np.ones(N), 1); y = rng.normal(5e-4, 0.015, (1, H, N)).astype(np.float32)
 L = _lib.load()
-L.kmpc_solve_trace.argtypes = [ctypes.POINTER(_lib.SolveDesc)] + [ctypes.c_void_p] * 8
+L.kmpc_solve_trace.argtypes = [ctypes.POINTER(_lib.SolveDesc)] + [ctypes.c_void_p] * 8 + [ctypes.c_size_t, ctypes.c_void_p]
 d = _solve_desc(1, N, H, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau), True)
 yt = torch.tensor(y, device="cuda"); wt = torch.tensor(wp, device="cuda")
 W = torch.empty((1, H, N), dtype=torch.float64, device="cuda"); st = torch.empty(1, dtype=torch.int32, device="cuda")
 ob = torch.empty(1, dtype=torch.float64, device="cuda"); it = torch.empty(1, dtype=torch.int32, device="cuda")
 tr = torch.full((4 * 100,), float("nan"), dtype=torch.float64, device="cuda")
-rc = L.kmpc_solve_trace(ctypes.byref(d), yt.data_ptr(), wt.data_ptr(), W.data_ptr(), st.data_ptr(), ob.data_ptr(), it.data_ptr(), tr.data_ptr(), None)
+nws = int(L.kmpc_workspace_bytes(None, ctypes.byref(d)))
+ws = torch.empty(max(nws, 8), dtype=torch.uint8, device="cuda")
+rc = L.kmpc_solve_trace(ctypes.byref(d), yt.data_ptr(), wt.data_ptr(), W.data_ptr(), st.data_ptr(), ob.data_ptr(), it.data_ptr(), tr.data_ptr(), ws.data_ptr(), nws, None)
 torch.cuda.synchronize()
 print("rc", rc, "status", st.item(), "iters", it.item(), "obj", ob.item())
 t = tr.cpu().numpy().reshape(-1, 4)
