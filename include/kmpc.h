@@ -61,6 +61,10 @@ extern "C" {
  *          return_full_W != 0; status [B]; obj [B] (problem.value, NaN when not optimal);
  *          iters [B] (may be NULL).
  * Failure fallback (mpc.py:113-115) is applied in-kernel: w_out = tile(w_prev), obj = NaN.
+ * Workspace: kmpc_workspace_bytes(NULL, desc) bytes (0 for windows of N <= 256 assets and
+ *          H <= 10 periods, solved in registers; otherwise the large-window kernel keeps each
+ *          window's interior-point state there, ~ (22 H + 128) (64 ceil(N / 64)) doubles per
+ *          window for min(B, 512) windows in flight). Too little -> KMPC_ERR_WORKSPACE.
  */
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
@@ -227,7 +231,8 @@ int kmpc_rolling_moments(int B, int T, int N, int lookback, const float* z, int 
                          const float* mean, const float* std, const int* ts,
                          double* mu, double* sigma, int* valid, void* stream);
 
-/* Workspace needed by kmpc_rollout / kmpc_solve / kmpc_window (either desc may be NULL). */
+/* Workspace needed by kmpc_rollout / kmpc_solve / kmpc_window (either desc may be NULL; with both,
+   the sum for kmpc_window: rollout scratch + yhat + the solve's). */
 size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc);
 
 /* Human-readable text for a return code or (status + 100) for a per-problem status. */

@@ -78,10 +78,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     if (a.H <= 5) return launch_ipm<5>(a, stream);
 #endif
     if (a.H <= 10) return launch_ipm<10>(a, stream);
-#ifndef KMPC_DEV_ONLY_H10
-    if (a.H <= 21) return launch_ipm<21>(a, stream);
-#endif
-    return KMPC_ERR_UNSUPPORTED;
+    return KMPC_ERR_UNSUPPORTED;   // H > 10: the large-window kernel
 }
 
 }  // namespace kmpc

@@ -40,12 +40,17 @@ constexpr int LDG = 65;            // LDS row stride of G / L (conflict-free row
 constexpr int NWX = 16;            // max waves per window (1024 threads)
 constexpr int MAX_SLOTS = 512;     // windows in flight = workspace slabs
 constexpr double LR_FLOOR = 1e-14;
+#ifndef KMPC_BIG_WPE
+#define KMPC_BIG_WPE 1
+#endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // per-(t, i) arrays of a window's slab (assets contiguous)
+// (P, BP = bma P and BMA are this iteration's s-elimination coefficients, written by the factor pass
+// so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
-             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, N_ARR };
+             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, A_BMA, N_ARR };
 
 __host__ __device__ inline size_t slab_doubles(int HM, int NP) {
     return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
@@ -140,6 +145,7 @@ struct Win {
     }
     __device__ __forceinline__ double alpha(int t, double m) const { return m * sh.iden[t] * irsig; }
     __device__ __forceinline__ double eps(int t, const St& e) const { return ht() ? sh.sr[t] * e.bma * e.P : 0.0; }
+    __device__ __forceinline__ double epsa(int t) const { return ht() ? sh.sr[t] * at(A_BP, t) : 0.0; }
 
     // ---- reductions ----
     // wave total of v into this wave's partial slot j (every lane of the wave must call)
@@ -241,6 +247,9 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             mu_l += r1 + r2 + r3;
             rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
             P = cur.P;
+            W.at(A_P, t) = cur.P;
+            W.at(A_BP, t) = cur.bma * cur.P;
+            W.at(A_BMA, t) = cur.bma;
             W.at(A_RC1, t) = r1;
             W.at(A_RC2, t) = r2;
             W.at(A_RC3, t) = r3;
@@ -314,15 +323,13 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
         frexp(pi, &e);
     }
     const double cen = ldexp(1.0, -(e / 2));
-    double wprev = W.wpi, pi = 1.0, gp = 0.0, bp = 0.0, dqp = 0.0;
+    double pi = 1.0, gp = 0.0, bp = 0.0, dqp = 0.0;
     for (int t = 0; t < H; ++t) {
         double vv = 0.0;
         if (W.act) {
-            const St s = W.st(t, wprev);
-            wprev = s.w;
             const double lr = W.at(A_LR, t), dq = W.at(A_X, t);
             if (t) pi *= fmax(lr, LR_FLOOR);
-            const double al = W.alpha(t, s.m), ep = W.eps(t, s);
+            const double al = W.alpha(t, W.at(A_M, t)), ep = W.epsa(t);
             const double pt = pi * cen, gt = 1.0 / pt, bt = dq * pt;
             W.lg(3 * t)[W.i] = ep * (gt - gp);
             W.lg(3 * t + 1)[W.i] = al * gt;
@@ -502,19 +509,13 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
         if (W.act) {
             // rhs_w -= g_t - g_{t+1}, g = bma P (bs - rho px); forward sweep y_t = x_t + Lr_t y_{t-1} (Y)
             double y = 0.0;
-            St cur = W.st(0, W.wpi);
-            double gc = hs ? cur.bma * cur.P * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
+            double gc = hs ? W.at(A_BP, 0) * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
             for (int t = 0; t < H; ++t) {
                 double gn = 0.0;
-                St nxt = cur;
-                if (t + 1 < H) {
-                    nxt = W.st(t + 1, cur.w);
-                    gn = hs ? nxt.bma * nxt.P * (W.at(A_BS, t + 1) - sh.rho[t + 1] * sh.px[t + 1]) : 0.0;
-                }
+                if (hs && t + 1 < H) gn = W.at(A_BP, t + 1) * (W.at(A_BS, t + 1) - sh.rho[t + 1] * sh.px[t + 1]);
                 const double x = W.at(A_BW, t) - gc + gn;
                 y = x + W.at(A_LR, t) * y;
                 W.at(A_Y, t) = y;
-                cur = nxt;
                 gc = gn;
             }
         }
@@ -526,9 +527,8 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
             if (W.act) {
                 x = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * xn;
                 W.at(A_X, t) = x;
-                const St s = W.st(t, W.wprev(t));
-                ep = W.eps(t, s);
-                va = W.alpha(t, s.m) * x;
+                ep = W.epsa(t);
+                va = W.alpha(t, W.at(A_M, t)) * x;
                 vv1 = (t + 1 < H) ? epn * (xn - x) : 0.0;
                 lrn = W.at(A_LR, t);
             }
@@ -547,20 +547,13 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
         if (W.act) {
             // Z q per period: alpha_t q_a + q_1 + eps_t q_v(t) - eps_{t+1} q_v(t+1); forward sweep (Y)
             double y = 0.0;
-            St cur = W.st(0, W.wpi);
-            double epc = W.eps(0, cur);
+            double epc = W.epsa(0);
             for (int t = 0; t < H; ++t) {
-                double epn = 0.0;
-                St nxt = cur;
-                if (t + 1 < H) {
-                    nxt = W.st(t + 1, cur.w);
-                    epn = W.eps(t + 1, nxt);
-                }
-                const double zq = W.alpha(t, cur.m) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
+                const double epn = (t + 1 < H) ? W.epsa(t + 1) : 0.0;
+                const double zq = W.alpha(t, W.at(A_M, t)) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
                                   ((t + 1 < H) ? epn * sh.q[3 * t + 3] : 0.0);
                 y = zq + W.at(A_LR, t) * y;
                 W.at(A_Y, t) = y;
-                cur = nxt;
                 epc = epn;
             }
         }
@@ -574,20 +567,20 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
                 lrn = W.at(A_LR, t);
                 const double dw = W.at(A_X, t) - tq;
                 if (first) W.at(A_DW, t) = dw; else W.at(A_DW, t) += dw;
-                const St s = W.st(t, W.wprev(t));
+                const double bma = hs ? W.at(A_BMA, t) : 0.0, P = hs ? W.at(A_P, t) : 0.0;
                 if (hs && t + 1 < H) {
                     const double bs = W.at(A_BS, t + 1) - bman * (dwn - dw);
                     W.at(A_BS, t + 1) = bs;
                     pxn = Pn * bs;
                 }
                 if (hs && t == 0) {
-                    const double bs = W.at(A_BS, 0) - s.bma * dw;
+                    const double bs = W.at(A_BS, 0) - bma * dw;
                     W.at(A_BS, 0) = bs;
-                    px0 = s.P * bs;
+                    px0 = P * bs;
                 }
                 dwn = dw;
-                bman = s.bma;
-                Pn = s.P;
+                bman = bma;
+                Pn = P;
             }
             if (t + 1 < H) W.slot(t + 1, pxn);
             if (t == 0) W.slot(0, px0);
@@ -598,11 +591,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
     {
         if (W.act) {
             for (int t = 0; t < H; ++t) {
-                double ds = 0.0;
-                if (hs) {
-                    const St s = W.st(t, W.wprev(t));
-                    ds = s.P * (W.at(A_BS, t) - sh.rho[t] * sh.tot[t]);
-                }
+                const double ds = hs ? W.at(A_P, t) * (W.at(A_BS, t) - sh.rho[t] * sh.tot[t]) : 0.0;
                 if (first) W.at(A_DS, t) = ds; else W.at(A_DS, t) += ds;
             }
         }
@@ -906,7 +895,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
 }
 
 template <int HM, int MAXT, int FL>
-__global__ void __launch_bounds__(MAXT) ipm_big(BigArgs A) {
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(KMPC_BIG_WPE))) ipm_big(BigArgs A) {
     static_assert(3 * HM <= KP - 1, "Schur system must fit one wave");
     __shared__ BigShared<HM> sh;
     const SolveArgs& a = A.s;

@@ -1595,9 +1595,8 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
     if (nt <= 64) return exact ? launch_one<HM, 64, true, -1>(a, nt, stream) : launch_one<HM, 64, false, -1>(a, nt, stream);
     if (nt <= 128) return exact ? launch_one<HM, 128, true, -1>(a, nt, stream) : launch_one<HM, 128, false, -1>(a, nt, stream);
     if (nt <= 256) return exact ? launch_one<HM, 256, true, -1>(a, nt, stream) : launch_one<HM, 256, false, -1>(a, nt, stream);
-    // two waves per SIMD: 256 registers per thread (the 1024-thread variant has 128)
-    if (nt <= 512) return launch_one<HM, 512, false, -1>(a, nt, stream);
-    return launch_one<HM, 1024, false, -1>(a, nt, stream);
+    // past 256 assets a window's state does not fit the registers of one block: kmpc_solve_big.h
+    return KMPC_ERR_UNSUPPORTED;
 }
 
 // Constant-case launcher (H == HM, N <= 128): the constraint case is a template argument, so every
