@@ -200,9 +200,12 @@ int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, do
  * with w_{-1} = w_prev. mu [B,H,N] float64 (the reference passes predicted log-returns / the
  * Markowitz rolling mean as mu), Sigma [B,N,N] float64 (sigma_stride = N*N) or one shared [N,N]
  * (sigma_stride = 0). Outputs as kmpc_solve; failure fallback tile(w_prev), obj = NaN
- * (mpc.py:180-181). Shapes: H*N <= KMPC_MV_MAX_HN, H <= KMPC_MV_MAX_H.
+ * (mpc.py:180-181). Shapes: H*N <= KMPC_MV_MAX_HN, H <= KMPC_MV_MAX_H. Past H*N = 128 the
+ * dense Newton matrix leaves LDS for a workspace slab (kmpc_mv_workspace_bytes; use
+ * kmpc_solve_mv_ws — kmpc_solve_mv, which has no workspace argument, then returns
+ * KMPC_ERR_WORKSPACE).
  */
-#define KMPC_MV_MAX_HN 128
+#define KMPC_MV_MAX_HN 1024
 #define KMPC_MV_MAX_H  16
 typedef struct kmpc_mv_desc {
     int    B, N, H;
@@ -220,6 +223,11 @@ int kmpc_solve_mv(const kmpc_mv_desc* desc,
                   size_t sigma_stride,     /* elements between windows' Sigma (0: shared) */
                   const double* w_prev,    /* [B,N] */
                   double* w_out, int* status, double* obj, int* iters, void* stream);
+/* kmpc_solve_mv with a caller-provided workspace of kmpc_mv_workspace_bytes(desc) bytes */
+size_t kmpc_mv_workspace_bytes(const kmpc_mv_desc* desc);
+int kmpc_solve_mv_ws(const kmpc_mv_desc* desc, const double* mu, const double* sigma, size_t sigma_stride,
+                     const double* w_prev, double* w_out, int* status, double* obj, int* iters,
+                     void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- Markowitz rolling moments: MarkowitzStrategy.rebalance (baselines.py:70-88) ------------ */
 /* For window b at test row t = ts[b]: returns r_s = z_s * std + mean (float32, as

@@ -27,12 +27,13 @@ DTYPE = {"fp32": 0, "bf16": 1}
 STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
                 4: "solver_error"}
 
-KMPC_MV_MAX_HN = 128     # mean-variance solve: H * N per workgroup
+KMPC_MV_MAX_HN = 1024    # mean-variance solve: H * N per workgroup (> 128: workspace-resident matrix)
 KMPC_MV_MAX_H = 16
 
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
                     "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_standardize", "kmpc_strerror",
-                    "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments")
+                    "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments", "kmpc_solve_mv_ws",
+                    "kmpc_mv_workspace_bytes")
 
 
 class KmpcError(RuntimeError):
@@ -102,6 +103,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_standardize.restype = ctypes.c_int
     L.kmpc_solve_mv.argtypes = [ctypes.POINTER(MvDesc), vp, vp, sz, vp, vp, vp, vp, vp, vp]
     L.kmpc_solve_mv.restype = ctypes.c_int
+    L.kmpc_solve_mv_ws.argtypes = [ctypes.POINTER(MvDesc), vp, vp, sz, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.kmpc_solve_mv_ws.restype = ctypes.c_int
+    L.kmpc_mv_workspace_bytes.argtypes = [ctypes.POINTER(MvDesc)]
+    L.kmpc_mv_workspace_bytes.restype = ctypes.c_size_t
     ci = ctypes.c_int
     L.kmpc_rolling_moments.argtypes = [ci, ci, ci, ci, vp, ci, vp, vp, vp, vp, vp, vp, vp]
     L.kmpc_rolling_moments.restype = ctypes.c_int

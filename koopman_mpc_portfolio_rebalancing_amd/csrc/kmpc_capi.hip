@@ -130,12 +130,21 @@ extern "C" {
 int kmpc_solve_mv(const kmpc_mv_desc* desc, const double* mu, const double* sigma, size_t sigma_stride,
                   const double* w_prev, double* w_out, int* status, double* obj, int* iters,
                   void* stream) {
+    return kmpc_solve_mv_ws(desc, mu, sigma, sigma_stride, w_prev, w_out, status, obj, iters, nullptr, 0,
+                            stream);
+}
+
+size_t kmpc_mv_workspace_bytes(const kmpc_mv_desc* desc) { return kmpc::mv_workspace_bytes(desc); }
+
+int kmpc_solve_mv_ws(const kmpc_mv_desc* desc, const double* mu, const double* sigma, size_t sigma_stride,
+                     const double* w_prev, double* w_out, int* status, double* obj, int* iters,
+                     void* workspace, size_t ws_bytes, void* stream) {
     if (!desc || desc->B < 0 || desc->N < 1 || desc->H < 1) return KMPC_ERR_INVALID;
     if (desc->H > KMPC_MV_MAX_H || desc->N * desc->H > KMPC_MV_MAX_HN) return KMPC_ERR_UNSUPPORTED;
     if (desc->B == 0) return KMPC_OK;
     if (!mu || !sigma || !w_prev || !w_out || !status || !obj) return KMPC_ERR_INVALID;
-    return kmpc::mv_solve_launch(desc, mu, sigma, sigma_stride, w_prev, w_out, status, obj, iters,
-                                 (hipStream_t)stream);
+    return kmpc::mv_solve_launch(desc, mu, sigma, sigma_stride, w_prev, w_out, status, obj, iters, workspace,
+                                 ws_bytes, (hipStream_t)stream);
 }
 
 int kmpc_rolling_moments(int B, int T, int N, int lookback, const float* z, int ldz,

@@ -28,9 +28,10 @@ int standardize_launch(int T, int N, const double* y, const double* mean, const 
 
 // kmpc_mv.hip
 size_t mv_lds_bytes(int N, int H);
+size_t mv_workspace_bytes(const kmpc_mv_desc* d);
 int mv_solve_launch(const kmpc_mv_desc* d, const double* mu, const double* sigma, size_t sigma_stride,
                     const double* w_prev, double* w_out, int* status, double* obj, int* iters,
-                    hipStream_t stream);
+                    void* ws, size_t ws_bytes, hipStream_t stream);
 int rolling_moments_launch(int B, int T, int N, int lookback, const float* z, int ldz, const float* mean,
                            const float* stdv, const int* ts, double* mu, double* sigma, int* valid,
                            hipStream_t stream);

@@ -4,7 +4,7 @@
 // Program per window (mpc.py:128, 145-172):
 //   maximize  sum_t [ w_t . mu_t - gamma w_t' Sigma w_t ] - c sum_t ||w_t - w_{t-1}||_1
 //   s.t.      1'w_t = 1, w_t >= 0 unless allow_short          (no turnover cap), w_{-1} = w_prev.
-// One workgroup per window, one element (t, i) of W per thread (n = H N <= 128). Algorithm:
+// One workgroup per window, one element (t, i) of W per thread (n = H N <= 1024). Algorithm:
 // Mehrotra predictor-corrector primal-dual interior point on the epigraph form (s_ti >= |d_ti|,
 // d = w_t - w_{t-1}), float64, objective scaled by max(|mu|, 2 gamma |Sigma|, c). The s rows and
 // all multipliers are eliminated per element, leaving the dense SPD system
@@ -12,6 +12,9 @@
 // (D: differencing in t, E = 4 alpha beta / (alpha + beta) from the two |d| rows), solved with a
 // right-looking Cholesky of M in LDS (thread r owns row r) and the H x H Schur complement
 // S = A M^{-1} A' for the budget multipliers. Test-side restatement: oracle/mv_ref.py.
+// Storage: M (n x n) and M^{-1} A' sit in LDS while they fit (n <= 128); past that in a per-block
+// slab of the caller's workspace (L2-resident: 2 MB at n = 500), with a persistent grid of
+// min(B, MV_SLOTS) blocks walking the windows.
 //
 // Status / fallback as mpc.py:180-181: non-optimal -> W = tile(w_prev), obj = NaN.
 #include <hip/hip_runtime.h>
@@ -36,7 +39,11 @@ struct MvArgs {
     int* status;
     double* obj;
     int* iters;
+    double* ws;             // workspace slabs (global-M variant)
+    size_t slab;            // doubles per slab
 };
+
+constexpr int MV_SLOTS = 512;   // windows in flight of the global-M variant
 
 __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -128,22 +135,22 @@ __device__ double chol_solve(const double* M, int n, int np, double b, double* v
     return out;
 }
 
-template <int MAXT>
-__global__ void __launch_bounds__(MAXT) mv_ipm_kernel(MvArgs a) {
-    extern __shared__ double lds[];
+// One window. GM: M and Y in the block's workspace slab (else in LDS after the small arrays).
+template <bool GM>
+__device__ __forceinline__ void mv_window(const MvArgs& a, int b, double* lds) {
     const int N = a.N, H = a.H, n = N * H, np = n | 1;
-    double* M = lds;                        // [n][np] Newton matrix, then its Cholesky factor
-    double* vec = M + (size_t)n * np;       // [n] broadcast vector
-    double* Y = vec + n;                    // [H][n] M^{-1} A'
-    double* Sm = Y + (size_t)H * n;         // [H][H] A M^{-1} A', then its Cholesky factor
-    double* pv = Sm + H * H;                // [H] period sums
+    double* vec = lds;                      // [n] broadcast vector
+    double* Sm = vec + n;                   // [H][H] A M^{-1} A', then its Cholesky factor
+    double* M = GM ? a.ws + (size_t)blockIdx.x * a.slab : Sm + H * H + 4 * H + 18;   // [n][np]: M, then L
+    double* Y = M + (size_t)n * np;         // [H][n] M^{-1} A'
+    double* pv = Sm + H * H;                // [H] period sums (after Sm in LDS, both variants)
     double* nu = pv + H;                    // [H] budget multipliers
     double* dnu = nu + H;                   // [H]
     double* rpv = dnu + H;                  // [H] primal residuals 1'w_t - 1
-    double* red = rpv + H;                  // [2] reduction slots
-    int* flag = (int*)(red + 2);
+    double* red = rpv + H;                  // [16] reduction slots (one per wave)
+    int* flag = (int*)(red + 16);
 
-    const int b = blockIdx.x, k = threadIdx.x;
+    const int k = threadIdx.x;
     const bool act = k < n;
     const int t = act ? k / N : 0, i = act ? k - (k / N) * N : 0;
     const double* Sig = a.sigma + a.sigma_stride * (size_t)b;
@@ -369,6 +376,19 @@ __global__ void __launch_bounds__(MAXT) mv_ipm_kernel(MvArgs a) {
     }
 }
 
+template <int MAXT, bool GM>
+__global__ void __launch_bounds__(MAXT) mv_ipm_kernel(MvArgs a) {
+    extern __shared__ double lds[];
+    if (GM) {
+        for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+            mv_window<true>(a, b, lds);
+            __syncthreads();
+        }
+    } else {
+        mv_window<false>(a, blockIdx.x, lds);
+    }
+}
+
 // Markowitz moments (baselines.py:70-88) for window b at test index t = ts[b]:
 // r_s = z_s * std + mean (float32, data_finance.py:740-742) for the rows s of the last `lookback`
 // of [0, t]; mu = mean (float32, as np.mean of the float32 history), Sigma = np.cov (float64,
@@ -407,14 +427,28 @@ __global__ void rolling_moments_kernel(int B, int T, int N, int lookback, const 
 
 }  // namespace
 
+// LDS of the small arrays (vec, Sm, pv, nu, dnu, rpv, red, flag) and, for the LDS variant, M and Y
+size_t mv_small_bytes(int N, int H) {
+    return sizeof(double) * ((size_t)N * H + (size_t)H * H + 4 * (size_t)H + 18);
+}
 size_t mv_lds_bytes(int N, int H) {
     const size_t n = (size_t)N * H, np = n | 1;
-    return sizeof(double) * (n * np + n + H * n + (size_t)H * H + 4 * (size_t)H + 2) + 16;
+    return mv_small_bytes(N, H) + sizeof(double) * (n * np + H * n);
+}
+static bool mv_in_lds(int N, int H) { return (size_t)N * H <= 128 && mv_lds_bytes(N, H) <= 160 * 1024; }
+static size_t mv_slab(int N, int H) {
+    const size_t n = (size_t)N * H, np = n | 1;
+    return n * np + H * n;
+}
+size_t mv_workspace_bytes(const kmpc_mv_desc* d) {
+    if (!d || d->B <= 0 || mv_in_lds(d->N, d->H)) return 0;
+    const size_t slots = d->B < MV_SLOTS ? d->B : MV_SLOTS;
+    return sizeof(double) * mv_slab(d->N, d->H) * slots;
 }
 
 int mv_solve_launch(const kmpc_mv_desc* d, const double* mu, const double* sigma, size_t sigma_stride,
                     const double* w_prev, double* w_out, int* status, double* obj, int* iters,
-                    hipStream_t stream) {
+                    void* ws, size_t ws_bytes, hipStream_t stream) {
     MvArgs a;
     a.B = d->B; a.N = d->N; a.H = d->H;
     a.gamma = d->gamma; a.c = d->cost_coeff;
@@ -424,11 +458,17 @@ int mv_solve_launch(const kmpc_mv_desc* d, const double* mu, const double* sigma
     a.return_full = d->return_full_W;
     a.mu = mu; a.sigma = sigma; a.sigma_stride = sigma_stride; a.wp = w_prev;
     a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
+    a.ws = (double*)ws; a.slab = mv_slab(d->N, d->H);
     const int n = d->N * d->H;
     const int nt = 64 * ((n + 63) / 64);
-    const size_t lds = mv_lds_bytes(d->N, d->H);
-    if (lds > 160 * 1024) return KMPC_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((mv_ipm_kernel<128>), dim3(d->B), dim3(nt), lds, stream, a);
+    if (mv_in_lds(d->N, d->H)) {
+        hipLaunchKernelGGL((mv_ipm_kernel<128, false>), dim3(d->B), dim3(nt), mv_lds_bytes(d->N, d->H), stream, a);
+    } else {
+        if (n > 1024 || mv_small_bytes(d->N, d->H) > 160 * 1024) return KMPC_ERR_UNSUPPORTED;
+        if (!ws || ws_bytes < mv_workspace_bytes(d)) return KMPC_ERR_WORKSPACE;
+        const int grid = d->B < MV_SLOTS ? d->B : MV_SLOTS;
+        hipLaunchKernelGGL((mv_ipm_kernel<1024, true>), dim3(grid), dim3(nt), mv_small_bytes(d->N, d->H), stream, a);
+    }
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 

@@ -362,7 +362,6 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
         const double* pa = W.lg(16 * I + (lane & 15)) + (lane >> 4);
         const double* pb = W.rg(16 * J + (lane & 15)) + (lane >> 4);
         d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
         for (int k0 = 0; k0 < N4; k0 += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k0], pb[k0], acc, 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

@@ -52,18 +52,23 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
 _WS = {}   # solve workspaces per (device, HIP stream): calls on different streams never share one
 
 
-def _solve_workspace(d: _lib.SolveDesc, device: torch.device) -> Tuple[int, int]:
-    """(pointer, bytes) of a workspace large enough for the solve described by d (the large-window
-    kernel keeps each window's interior-point state there; the register kernels need none)."""
-    L = _lib.load()
-    nbytes = int(L.kmpc_workspace_bytes(None, ctypes.byref(d)))
-    if nbytes == 0:
-        return 0, 0
+def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """A device buffer of at least nbytes, cached per (device, current HIP stream)."""
     key = (device.index, _lib.stream_handle(device) or 0)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _WS[key] = ws
+    return ws
+
+
+def _solve_workspace(d: _lib.SolveDesc, device: torch.device) -> Tuple[int, int]:
+    """(pointer, bytes) of a workspace large enough for the solve described by d (the large-window
+    kernel keeps each window's interior-point state there; the register kernels need none)."""
+    nbytes = int(_lib.load().kmpc_workspace_bytes(None, ctypes.byref(d)))
+    if nbytes == 0:
+        return 0, 0
+    ws = _workspace(device, nbytes)
     return ws.data_ptr(), ws.numel()
 
 
@@ -200,9 +205,11 @@ def solve_mpc_mean_variance_batched(
     d.return_full_W = int(bool(return_full))
     L = _lib.load()
     with torch.cuda.device(dev):
-        rc = L.kmpc_solve_mv(ctypes.byref(d), mu64.data_ptr(), S.data_ptr(), stride, wp.data_ptr(),
-                             W.data_ptr(), status.data_ptr(), value.data_ptr(), iters.data_ptr(),
-                             _lib.stream_handle(dev))
+        nws = int(L.kmpc_mv_workspace_bytes(ctypes.byref(d)))
+        ws = _workspace(dev, nws) if nws else None
+        rc = L.kmpc_solve_mv_ws(ctypes.byref(d), mu64.data_ptr(), S.data_ptr(), stride, wp.data_ptr(),
+                                W.data_ptr(), status.data_ptr(), value.data_ptr(), iters.data_ptr(),
+                                ws.data_ptr() if ws is not None else None, nws, _lib.stream_handle(dev))
     _lib.check(rc)
     if with_iters:
         return W, status, value, iters

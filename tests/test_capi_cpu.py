@@ -51,7 +51,7 @@ def test_argument_errors_need_no_gpu():
     mv = _lib.MvDesc()
     mv.B, mv.N, mv.H = 1, 20, 0
     assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == -1
-    mv.H, mv.N = 1, 129                                       # H * N > KMPC_MV_MAX_HN
+    mv.H, mv.N = 1, 1025                                      # H * N > KMPC_MV_MAX_HN
     assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == -2
     mv.N, mv.B = 20, 0
     assert lib.kmpc_solve_mv(ctypes.byref(mv), None, None, 0, None, None, None, None, None, None) == 0

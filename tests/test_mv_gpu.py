@@ -64,6 +64,33 @@ def test_shared_sigma_and_drop_in_api():
         assert np.abs(Wb[b].cpu().numpy() - Wo[0]).max() < 1e-5
 
 
+@pytest.mark.parametrize("N,H,short", [(150, 1, False), (60, 3, False), (300, 2, False), (129, 1, True)])
+def test_mv_workspace_path_matches_oracle(N, H, short):
+    """H*N > 128: the Newton matrix no longer fits LDS and lives in a workspace slab (kmpc_mv.hip's
+    global-M kernel, persistent grid); same program, same tolerances as the golden cases."""
+    rng = np.random.default_rng(N * 10 + H)
+    B = 6
+    F = rng.standard_normal((B, N, 4)) * 0.02
+    sigma = F @ F.transpose(0, 2, 1) + np.eye(N) * 1e-4
+    mu = rng.standard_normal((B, H, N)) * 1e-3
+    wp = rng.dirichlet(np.ones(N), size=B)
+    cfg = MPCConfig(horizon=H, gamma=1.0, cost_coeff=1e-3, allow_short=short)
+    W, st, val = solve_mpc_mean_variance_batched(torch.tensor(wp, device=DEV), torch.tensor(mu, device=DEV),
+                                                 torch.tensor(sigma, device=DEV), cfg, return_full=True)
+    torch.cuda.synchronize()
+    W, st, val = W.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy()
+    assert (st == 0).all(), st
+    for b in range(B):
+        Wo, so = mv_ref.mv_dense_ipm(wp[b], mu[b], sigma[b], 1.0, 1e-3, allow_short=short)
+        assert so == "optimal"
+        fo = mv_ref.mv_objective(Wo, wp[b], mu[b], sigma[b], 1.0, 1e-3)
+        assert abs(val[b] - fo) <= 1e-9 + 1e-7 * abs(fo)
+        assert np.abs(W[b] - Wo).max() < 1e-5
+    assert np.abs(W.sum(-1) - 1).max() < 1e-9
+    if not short:
+        assert W.min() > -1e-9
+
+
 def test_fallbacks():
     """Non-finite input -> solver_error + tile(w_prev) and no "value" (mpc.py:180-181);
     allow_short with gamma = 0, c = 0 and a return spread is an unbounded LP."""

@@ -20,7 +20,7 @@ def mean(db, counter):
 
 
 out, B, fetch_db, write_db = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
-d = {"kernel": "ipm_kernel<10,128,true> (kmpc_solve)", "windows_per_launch": B,
+d = {"kernel": "ipm_kernel<10,128,true,7> (kmpc_solve, constant-case)", "windows_per_launch": B,
      "fetch_bytes_per_window": 2 * 1024 * mean(fetch_db, "FETCH_SIZE") / B,
      "write_bytes_per_window": 1024 * mean(write_db, "WRITE_SIZE") / B,
      "source": "rocprofv3 --pmc passes of `python bench.py --cpu-seconds 0 --steps 3 --warmup 1` (tools/gpu_round.sh)"}
