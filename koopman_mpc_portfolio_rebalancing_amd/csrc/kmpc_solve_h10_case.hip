@@ -5,3 +5,7 @@
 namespace kmpc {
 template int launch_ipm_case<10>(const SolveArgs& a, hipStream_t stream);
 }  // namespace kmpc
+
+#ifdef KMPC_STATS
+extern "C" int kmpc_debug_stats_case(unsigned long long* out, int reset) { return kmpc::debug_stats_tu(out, reset); }
+#endif

@@ -56,6 +56,22 @@ struct PhaseClock {
 };
 #define KMPC_PH_START(P) P.start()
 #define KMPC_PH(P, k) P.mark(k)
+// dev builds only (tools/phase_stats.py): out[0..1] = refinement steps, Newton solves;
+// out[2..17] = s_memtime cycles per solver phase. reset != 0 zeroes the counters afterwards.
+// Every solve translation unit has its own counters (no relocatable device code): each dev TU
+// exports its own copy of this reader.
+static int debug_stats_tu(unsigned long long* out, int reset) {
+    unsigned long long h[18];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(kmpc::g_stats), sizeof(unsigned long long) * 2) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(h + 2, HIP_SYMBOL(kmpc::g_phase), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    for (int k = 0; k < 18; ++k) out[k] = h[k];
+    if (reset) {
+        const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kmpc::g_stats), z, sizeof(unsigned long long) * 2) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kmpc::g_phase), z, sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    }
+    return 0;
+}
 #else
 struct PhaseClock {};
 #define KMPC_PH_START(P) (void)0
@@ -648,6 +664,14 @@ __device__ __forceinline__ double to_bound(double v, double dv, double a) {
     return (dv < 0.0) ? fmin(a, -v * r) : a;
 }
 
+// 1 / x for the per-asset reciprocals of factor(): v_rcp_f64 and two Newton steps (~1 ulp), a
+// third of the instructions of a correctly rounded f64 division (x > 0 finite on every use)
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+
 // Dual residuals of the current iterate (rows 1-2) at period t.
 template <int HM, int NWM, class TH>
 __device__ __forceinline__ void dual_residual(const TH& T, const Shared<HM, NWM>& sh, int t,
@@ -989,12 +1013,12 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         double iw = 0.0, iz2 = 0.0, iz3 = 0.0;
         if (T.act && t < H) {
             const double d = T.w[t] - T.wprev(t);
-            if (T.hw) { iw = 1.0 / T.w[t]; W1[t] = T.l1[t] * iw; }
+            if (T.hw) { iw = rcp_nr(T.w[t]); W1[t] = T.l1[t] * iw; }
             if (T.hs) {
-                iz2 = 1.0 / (T.s[t] - d);
-                iz3 = 1.0 / (T.s[t] + d);
+                iz2 = rcp_nr(T.s[t] - d);
+                iz3 = rcp_nr(T.s[t] + d);
                 const double al = T.l2[t] * iz2, be = T.l3[t] * iz3;
-                const double P = 1.0 / (al + be);
+                const double P = rcp_nr(al + be);
                 T.P[t] = P;
                 E[t] = 4.0 * al * be * P;
                 sp[t] = P;
@@ -1028,7 +1052,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                 }
                 const double dd = pi + ((t + 1 < HM && t + 1 < H) ? E[t + 1] : 0.0);
                 ok = ok && (dd > 0.0) && (dd < 1e300);
-                T.iDd[t] = 1.0 / dd;
+                T.iDd[t] = rcp_nr(dd);
             }
         }
     }
@@ -1221,24 +1245,27 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         double dinv = 0.0;
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
-            const double d = bcast(g[j], j);
+            const double u = g[j];                    // row r of the updated column j
+            // the column goes out first and its reads are issued before the pivot reciprocal:
+            // the v_rcp_f64 chain runs under the LDS round trip instead of ahead of it
+            double cv[KM];
+            if (j + 1 < KM) {
+                sh.col[r] = u;
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = j + 1; k < KM; ++k) cv[k] = sh.col[k];
+            }
+            const double d = bcast(u, j);
             bad = bad || !(d > 0.0) || !(d < 1e300);
-            // 1 / d: v_rcp_f64 + two Newton steps (~1 ulp; the chain is latency bound)
+            // 1 / d: v_rcp_f64 + two Newton steps (~1 ulp)
             const double dm = fmax(d, 1e-300);
             double id = __builtin_amdgcn_rcp(dm);
             id = fma(id, fma(-dm, id, 1.0), id);
             id = fma(id, fma(-dm, id, 1.0), id);
-            const double u = g[j];                    // row r of the updated column j
             const double l = (r > j) ? u * id : 0.0;  // L_rj
             if (r == j) dinv = id;
             g[j] = l;
             if (j + 1 < KM) {
-                sh.col[r] = u;
-                __builtin_amdgcn_wave_barrier();
-                // all reads of the column in flight at once (one LDS round trip per step)
-                double cv[KM];
-#pragma unroll
-                for (int k = j + 1; k < KM; ++k) cv[k] = sh.col[k];
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = j + 1; k < KM; ++k) g[k] = fma(-l, cv[k], g[k]);
@@ -1403,6 +1430,8 @@ __global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
                         ssum[t] = on ? T.s[t] : 0.0;
                         l1n[t] = on ? fabs(T.w[t] - T.wprev(t)) : 0.0;
                     }
+                    // (folding l1n into this reduction as a fourth array is slower: the 64-slot
+                    // reduce-scatter costs more than the separate one-barrier own1 below)
                     double o[4];
                     R.own3(mw, sw, ssum, o);
 #pragma unroll

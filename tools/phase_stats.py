@@ -3,6 +3,19 @@ import ctypes, glob, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from koopman_mpc_portfolio_rebalancing_amd import _lib, MPCConfig, solve_mpc_log_utility_batched
+
+
+def read_stats(L, reset=1):
+    """Sum of the dev counters of every solve translation unit that exports a reader."""
+    tot = [0] * 18
+    for fn in ("kmpc_debug_stats", "kmpc_debug_stats_case"):
+        if hasattr(L, fn):
+            f = getattr(L, fn)
+            f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+            st = (ctypes.c_ulonglong * 18)()
+            f(st, reset)
+            tot = [a + b for a, b in zip(tot, st)]
+    return tot
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 N, H = 100, 10
 rng = np.random.default_rng(0)
@@ -26,16 +39,14 @@ names = ["residual+best", "factor:prep", "factor:gram", "factor:chol", "newton",
 libs = sys.argv[2:] or sorted(os.path.basename(p) for p in glob.glob(os.path.join(os.path.dirname(_lib.LIB_PATH), "libkmpc_dev*.so")))
 for name in libs:
     L = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), name))
-    L.kmpc_debug_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     _lib._lib = L
     cfg = MPCConfig(horizon=H)
     solve_mpc_log_utility_batched(wp, y, cfg); torch.cuda.synchronize()
-    st = (ctypes.c_ulonglong * 18)()
-    L.kmpc_debug_stats(st, 1)
+    read_stats(L)
     t = time.time()
     W, s, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
     torch.cuda.synchronize(); dt = time.time() - t
-    L.kmpc_debug_stats(st, 1)
+    st = read_stats(L)
     nb = (B + 255) // 256
     iters = it.float().mean().item()
     tot = sum(st[2 + k] for k in range(7))
