@@ -9,9 +9,10 @@
 // H = 20, BASELINE configs[4]); ipm_kernel keeps it in registers (one asset per lane, every period
 // in VGPRs) and past 128 assets or 10 periods spills it to scratch. Here the state lives in a
 // per-window slab of the caller's workspace, [array][t][i] with the assets contiguous, so every
-// access is one coalesced wave load; each phase streams only the arrays it needs, and the
-// slack-derived quantities (reciprocals, P, the s-elimination coefficients) are recomputed from the
-// state instead of stored. The solve is bound by that HBM / Infinity-Cache stream.
+// access is one coalesced wave load; each phase streams only the arrays it needs. The slack
+// reciprocals are recomputed from the state where they are used; the s-elimination coefficients
+// (P, bma P, bma) are written once per iteration by the factor pass and read by the Newton passes.
+// The solve is bound by that HBM / Infinity-Cache stream.
 //
 // Layout: one workgroup per window, one asset per thread (blockDim = 64 ceil(N / 64) <= 1024), a
 // persistent grid of min(B, MAX_SLOTS) workgroups walks the windows (workspace = slots x slab).

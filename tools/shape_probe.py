@@ -18,7 +18,11 @@ def run(name, B, N, H, cost, tau, reps=2):
     print(f"{name}: B={B} N={N} H={H} {dt*1e3:.1f} ms {B/dt:.0f} windows/s iters {it.float().mean().item():.1f} "
           f"status {np.bincount(st.cpu().numpy(), minlength=5)}", flush=True)
 
-run("C2", 4096, 30, 5, 0.0, 0.0)
-run("C1-shape", 4096, 10, 5, 1e-3, 0.2)
-run("C3", 16384, 100, 10, 1e-3, 0.2)
-run("C5", int(sys.argv[1]) if len(sys.argv) > 1 else 1024, 500, 20, 1e-3, 0.2, reps=1)
+run("C2", 65536, 30, 5, 0.0, 0.0)
+run("C1-shape", 65536, 10, 5, 1e-3, 0.2)
+run("C3", 65536, 100, 10, 1e-3, 0.2)
+run("N=250,H=10", 8192, 250, 10, 1e-3, 0.2)
+run("N=500,H=10", 4096, 500, 10, 1e-3, 0.2)
+run("N=100,H=20", 8192, 100, 20, 1e-3, 0.2)
+run("N=1000,H=5", 2048, 1000, 5, 1e-3, 0.2)
+run("C5", int(sys.argv[1]) if len(sys.argv) > 1 else 2048, 500, 20, 1e-3, 0.2, reps=2)
