@@ -77,6 +77,12 @@ struct PhaseClock {};
 #define KMPC_PH_START(P) (void)0
 #define KMPC_PH(P, k) (void)0
 #endif
+// Horizon bounds up to this one run two waves per SIMD (amdgpu_waves_per_eu(2): 256 registers per
+// lane, a few dozen dwords spilled for the turnover case) — measured on C1-shaped windows (N = 10,
+// H = 5): 3.9 M -> 5.7 M windows/s; the H = 10 kernels need ~660 live dwords and stay at one.
+#ifndef KMPC_WPE2_HM
+#define KMPC_WPE2_HM 5
+#endif
 #ifndef KMPC_REFINE_RTOL
 #define KMPC_REFINE_RTOL 1e-7
 #endif
@@ -289,22 +295,24 @@ struct Shared {
     static constexpr int KM = 3 * HM;
     static constexpr int MC = pow2_at_least(KM);          // Schur chunk width (one G column)
     static constexpr int RW = max_i(3 * MC, 64);          // reduction slots per wave
+    // One-wave windows (NWM = 1) drop L's transposed copy and the second reduction buffer (one
+    // wave cannot overrun its own slot reads), so four one-wave windows fit a CU's 160 KB.
+    static constexpr bool LT = NWM > 1;
+    static constexpr int NB = NWM > 1 ? 2 : 1;
     union {
         struct {
             double G[KM * KM];  // Schur matrix, then L of G = L D L^T (strictly lower, row-major)
-            double Lt[KM * KM]; // L transposed (column-contiguous reads in the forward solve)
+            double Lt[LT ? KM * KM : 1]; // L transposed (column-contiguous reads in the forward solve)
         };
-        double gred[2 * KM * KM];   // static-slot Gram: per-wave partial sums [wave][slot]
+        double gred[static_gram<HM, NWM>() ? NWM * gram_slots(HM) : 1];   // static-slot Gram: per-wave partial sums [wave][slot]
     };
     double gid[KM];             // 1 / D_jj
-    double col[WAVE];           // LDL^T: the current column, broadcast to the factoring wave
     double bs[KM];              // Schur right-hand side, then solution q
-    double red[2][NWM][RW];     // double-buffered reduction slots
+    double red[NB][NWM][RW];    // double-buffered reduction slots (also the LDL^T column broadcast)
     // per-period scalars
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM];
     double rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
-    double t_adw[HM], t_sds[HM], t_sdw[HM];
     double best_rw[HM], best_l1[HM];   // per-period R.w and ||w_t - w_{t-1}||_1 of the best iterate
     int flag;
 };
@@ -440,7 +448,7 @@ struct Reducer {
                 v[j0 + j] = s;
             }
         }
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
     }
     // per-period sums of up to three [HM] arrays in one reduction
     __device__ __forceinline__ void periods(double (&a)[HM]) {
@@ -509,7 +517,7 @@ struct Reducer {
             for (int q = 1; q < NWM; ++q) sum += tmp[q][k];
             out[k] = sum;
         }
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
     }
     __device__ __forceinline__ double own1(const double (&a)[HM]) {
         constexpr int M = pow2_at_least(HM);
@@ -585,7 +593,7 @@ struct Reducer {
 #pragma unroll
         for (int q = 1; q < NWM; ++q)
             if (q < nw) m = fmin(m, t0[q][HM]);
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
         return m;
     }
     // block sum of s and block maximum of mx, sharing one barrier
@@ -610,7 +618,7 @@ struct Reducer {
             S += ss[q];
             if (q < nw) MX = fmax(MX, mm[q]);
         }
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
     }
     __device__ __forceinline__ double sum1(double x) {
         const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
@@ -623,7 +631,7 @@ struct Reducer {
 #pragma unroll
         for (int q = 0; q < NWM; ++q)
             if (q < nw) s += r[q * RW];
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
         return s;
     }
     __device__ __forceinline__ double max1(double x) {
@@ -637,7 +645,7 @@ struct Reducer {
 #pragma unroll
         for (int q = 1; q < NWM; ++q)
             if (q < nw) s = fmax(s, r[q * RW]);
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
         return s;
     }
     __device__ __forceinline__ double min1(double x) {
@@ -651,7 +659,7 @@ struct Reducer {
 #pragma unroll
         for (int q = 1; q < NWM; ++q)
             if (q < nw) s = fmin(s, r[q * RW]);
-        buf ^= 1;
+        buf ^= Shared<HM, NWM>::NB - 1;
         return s;
     }
 };
@@ -742,7 +750,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
             if ((lane & ((WAVE / MP) - 1)) == 0) rb[wv * RW + k * MP + slot] = v[0];
         }
         __syncthreads();
-        R.buf ^= 1;
+        R.buf ^= Shared<HM, NWM>::NB - 1;
         KMPC_PH(lp, 9);
         // wave 0: q = G^{-1} (bs - [0; 0; b6]) by forward / back substitution; lane r owns row r
         if (threadIdx.x < WAVE) {
@@ -763,7 +771,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
             {
                 double lf[KM - 1];
 #pragma unroll
-                for (int j = 0; j < KM - 1; ++j) lf[j] = sh.Lt[j * KM + lr];
+                for (int j = 0; j < KM - 1; ++j) lf[j] = Shared<HM, NWM>::LT ? sh.Lt[j * KM + lr] : sh.G[lr * KM + j];
                 const double gd = sh.gid[lr];
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1218,7 +1226,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                     }
                 }
             }
-            R.buf ^= 1;
+            R.buf ^= Shared<HM, NWM>::NB - 1;
     #pragma unroll
             for (int r = 0; r < HM; ++r) qp[r] = qc[r];
         }
@@ -1230,6 +1238,8 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     // column j through LDS (one ds_write, uniform-address reads: in order within the wave, no
     // barrier). Unused columns (t >= H, or the cap columns without a cap) become identity rows;
     // I' adds 1 on the a- and v-type diagonals. L is stored strictly lower (zero elsewhere).
+    // (the column broadcast of the LDL^T steps uses reduction slots: no reduction is in flight here)
+    double* col = &sh.red[0][0][0];
     if (threadIdx.x < WAVE) {
         const int r = lane;
         const bool rused = r < KM && (r % HM) < H && (r / HM != 1 || T.ht);
@@ -1250,10 +1260,10 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
             // the v_rcp_f64 chain runs under the LDS round trip instead of ahead of it
             double cv[KM];
             if (j + 1 < KM) {
-                sh.col[r] = u;
+                col[r] = u;
                 __builtin_amdgcn_wave_barrier();
 #pragma unroll
-                for (int k = j + 1; k < KM; ++k) cv[k] = sh.col[k];
+                for (int k = j + 1; k < KM; ++k) cv[k] = col[k];
             }
             const double d = bcast(u, j);
             bad = bad || !(d > 0.0) || !(d < 1e300);
@@ -1277,7 +1287,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
             for (int k = 0; k < KM; ++k) {
                 const double v = k < r ? g[k] : 0.0;
                 sh.G[r * KM + k] = v;
-                sh.Lt[k * KM + r] = v;
+                if constexpr (Shared<HM, NWM>::LT) sh.Lt[k * KM + r] = v;
             }
             sh.gid[r] = dinv;
         }
@@ -1314,7 +1324,7 @@ __device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM>& R, 
 
 // EXACT: H == HM known at compile time (all period predicates fold away).
 template <int HM, int MAXT, bool EXACT, int FL = -1>
-__global__ void __launch_bounds__(MAXT) ipm_kernel(SolveArgs args) {
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <= KMPC_WPE2_HM ? 2 : 1))) ipm_kernel(SolveArgs args) {
     static_assert(3 * HM <= WAVE, "Schur system must fit one wave");
     constexpr int NWM = MAXT / WAVE;
     __shared__ Shared<HM, NWM> sh;
