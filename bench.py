@@ -183,6 +183,37 @@ def cpu_baseline_serial(sd, mean, std, x_gpu, wp_gpu, H, N, cfg, budget_s):
                       f"1 thread, {dt:.1f} s"}
 
 
+def secondary_c2(dev, steps: int, warmup: int) -> dict:
+    """BASELINE configs[1] beside the headline (same step, same timing rule, rank 0 only): 4,096
+    windows, 30 assets, latent 128, H = 5, c = tau = 0 no-short (the simplex program)."""
+    from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
+                                                       solve_mpc_log_utility_batched)
+    B, N, L, H, hidden = 4096, 30, 128, 5, 1024
+    obs = N * 20
+    model = DeviceKoopman(KoopmanModelSpec.from_state_dict(make_state_dict(obs, L, hidden, seed=1), MODEL_CFG), dev)
+    mean_d = torch.full((N,), 5e-4, dtype=torch.float32, device=dev)
+    std_d = torch.full((N,), 0.015, dtype=torch.float32, device=dev)
+    x, wp = make_inputs(B, N, obs, seed=100, device=dev)
+    cfg = MPCConfig(horizon=H, cost_coeff=0.0, max_turnover=0.0, allow_short=False)
+    reps = 20 * max(steps, 1)
+
+    def step():
+        y = model.rollout(x, mean_d, std_d, H, N)
+        return solve_mpc_log_utility_batched(wp, y, cfg)
+    for _ in range(max(warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        W0, st, val = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": f"C2 (BASELINE configs[1]): {B} windows, {N} assets, latent {L}, H={H}, obs {obs}, "
+                        f"enc [{hidden},{hidden}], c=0 tau=0 no-short", "windows_per_s": B * reps / el,
+            "ms_per_step": el / reps * 1e3, "steps": reps,
+            "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -301,6 +332,8 @@ def main():
             "solver": {"optimal_or_inaccurate": n_opt, "windows": B,
                        "mean_ipm_iterations": float(its.float().mean().item())},
         }
+        if world == 1:
+            line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base

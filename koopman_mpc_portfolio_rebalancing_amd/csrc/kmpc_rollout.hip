@@ -55,7 +55,9 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     return gelu_erf(x);
 }
 
-// Tile: 128 x 128 outputs per 256-thread block (4 waves, 2 x 2 of 64 x 64), BK = 32.
+// Tile: 64 WT x 64 WT outputs per 256-thread block (4 waves, 2 x 2 of 32 WT x 32 WT), BK = 32.
+// WT = 2 (128 x 128) for large batches; WT = 1 (64 x 64) when 128-tiles would leave the 256 CUs
+// with fewer than two workgroups each (small window batches: configs[1]'s 4,096 windows).
 constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
 
 // C = epi(A . B^T). Each lane of an MFMA consumes 16 contiguous k (k = 16h + s, h = lane >> 5),
@@ -68,15 +70,16 @@ __device__ __forceinline__ float destandardize(float y, float sd, float mu) {
     return p + mu;
 }
 
-// fused epilogue of a 2 x 2 block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D layout
-// is dtype-independent on gfx950)
-__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0, int wm, int wn,
+// fused epilogue of a WT x WT block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D
+// layout is dtype-independent on gfx950)
+template <int WT>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[WT][WT], int m0, int n0, int wm, int wn,
                                          int lane) {
     // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < WT; ++b) {
             const int n = n0 + wn + b * 32 + (lane & 31);
             if (n >= g.N) continue;
             const float bias = g.bias ? g.bias[n] : 0.0f;
@@ -104,36 +107,38 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[2][2],
 // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs by linear id,
 // so neighbouring tiles of one row panel of A would land in 8 different L2s. Renumber so that each
 // XCD gets a contiguous run of tiles (same A row panels): id -> (id % 8) * (total / 8) + id / 8.
-__device__ __forceinline__ void xcd_tile(int& m0, int& n0) {
+__device__ __forceinline__ void xcd_tile(int& m0, int& n0, int tm = BM, int tn = BN) {
     const int gx = gridDim.x, total = gridDim.x * gridDim.y;
     int id = blockIdx.y * gx + blockIdx.x;
     if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
-    m0 = (id / gx) * BM;
-    n0 = (id % gx) * BN;
+    m0 = (id / gx) * tm;
+    n0 = (id % gx) * tn;
 }
 
+template <int WT>
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
-    __shared__ float As[BM * LDS_STRIDE];
-    __shared__ float Bs[BN * LDS_STRIDE];
+    constexpr int TM = 64 * WT;
+    __shared__ float As[TM * LDS_STRIDE];
+    __shared__ float Bs[TM * LDS_STRIDE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int m0, n0;
-    xcd_tile(m0, n0);
-    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
-    f32x16 acc[2][2];
+    xcd_tile(m0, n0, TM, TM);
+    const int wm = (wv >> 1) * 32 * WT, wn = (wv & 1) * 32 * WT;
+    f32x16 acc[WT][WT];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < WT; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
     const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
                         ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
     for (int k0 = 0; k0 < g.K; k0 += BK) {
-        // stage A and B tiles: 128 rows x 32 k = 1024 float4 per operand, 4 per thread
+        // stage A and B tiles: TM rows x 32 k = 8 TM float4 per operand, TM / 32 per thread
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int idx = tid + q * 256;          // 0..1023
+        for (int q = 0; q < TM / 32; ++q) {
+            const int idx = tid + q * 256;          // 0..8 TM - 1
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int kk = k0 + c4;
             f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
@@ -155,9 +160,9 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
         }
         __syncthreads();
         const int r = lane & 31, h = lane >> 5;
-        float af[2][16], bf[2][16];
+        float af[WT][16], bf[WT][16];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
+        for (int a = 0; a < WT; ++a) {
             const float* pa = As + (wm + a * 32 + r) * LDS_STRIDE + 16 * h;
             const float* pb = Bs + (wn + a * 32 + r) * LDS_STRIDE + 16 * h;
 #pragma unroll
@@ -171,13 +176,13 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
 #pragma unroll
         for (int s = 0; s < 16; ++s)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < WT; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
+                for (int b = 0; b < WT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         __syncthreads();
     }
-    epilogue(g, acc, m0, n0, wm, wn, lane);
+    epilogue<WT>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // bf16 variant (BASELINE configs[4]: "bf16 MFMA rollout"): the same 128 x 128 tile and epilogues;
@@ -247,7 +252,7 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
         }
         __syncthreads();
     }
-    epilogue(g, acc, m0, n0, wm, wn, lane);
+    epilogue<2>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
@@ -292,8 +297,14 @@ __global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
 static int gemm(const GemmArgs& g, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    if (g.bf16) hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL(gemm_nt_kernel, grid, dim3(256), 0, s, g);
+    if (g.bf16) {
+        hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
+    } else if ((size_t)grid.x * grid.y < 512) {
+        dim3 grid64((g.N + 63) / 64, (g.M + 63) / 64);
+        hipLaunchKernelGGL(gemm_nt_kernel<1>, grid64, dim3(256), 0, s, g);
+    } else {
+        hipLaunchKernelGGL(gemm_nt_kernel<2>, grid, dim3(256), 0, s, g);
+    }
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 
