@@ -326,6 +326,12 @@ def main():
                        "parallelism": f"windows sharded over {world} GPU(s), RCCL gather of W0"},
             "roofline": roof,
             "hbm_roofline": hbm,
+            # SURVEY.md §8(d)'s whole-path bound: compulsory bytes per window = obs (f32 N d) +
+            # w_prev + w0 (f32 as there), weights amortized: windows/s x bytes / 8 TB/s
+            "path_hbm_roofline": {"bound": "hbm", "bytes_per_window": 4 * obs + 8 * N,
+                                  "achieved": value / world * (4 * obs + 8 * N) / 1e9, "peak": HBM_PEAK / 1e9,
+                                  "unit": "GB/s", "frac": value / world * (4 * obs + 8 * N) / HBM_PEAK,
+                                  "ceiling_windows_per_s_per_gpu": HBM_PEAK / (4 * obs + 8 * N)},
             "kernels": {"rollout_ms": roll_ms, "solve_ms": solve_ms,
                         "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
                         "rollout_mfma_frac": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK},

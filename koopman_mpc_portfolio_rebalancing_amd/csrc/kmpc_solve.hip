@@ -5,6 +5,9 @@
 //     bound HM is instantiated in its own translation unit (kmpc_solve_h*.hip).
 //   ipm_big (kmpc_solve_big.h): the state in a workspace slab, streamed per phase, the Schur
 //     matrix on the f64 MFMA — for larger windows (N > 256 or H > 10), which need workspace.
+// Presolve: without turnover terms (c = tau = 0) and without shorting the program decouples into
+// one problem per period, max log(R_t . w_t) over the simplex, whose optimum is exact in closed
+// form (simplex_kernel below) — BASELINE configs[1], "no-short simplex projection only".
 #include "kmpc_internal.h"
 #include "kmpc_solve_args.h"
 
@@ -15,6 +18,62 @@ namespace {
 // solver path override (debug entry kmpc_debug_solver_path, tools/ A/B only): 0 = by shape,
 // 1 = register kernels whenever they support the shape, 2 = the large-window kernel
 int g_path = 0;
+
+bool simplex_case(const SolveArgs& a) {
+    return g_path == 0 && !(a.c > 0.0) && !(a.tau > 0.0) && !a.allow_short;
+}
+
+// c = tau = 0, w >= 0: per period t, log(R_t . w_t) with R = exp(yhat) > 0 is maximized over the
+// simplex exactly on the face of the assets with the largest yhat_t; the returned point is that
+// face's centre (equal weights over exact ties: the analytic centre an interior-point method
+// converges to, and the vertex e_argmax otherwise). problem.value as the IPM kernels report it
+// (mpc.py:103): sum_t log(R_t . w_t) - c sum_t ||w_t - w_{t-1}||_1 (c <= 0 here). One thread per
+// window: O(H N) loads and no iteration. Non-finite inputs -> solver_error and tile(w_prev).
+__global__ void __launch_bounds__(64) simplex_kernel(SolveArgs a) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
+    const float* y = a.yhat + (size_t)b * H * N;
+    const double* wp = a.wp + (size_t)b * N;
+    double* wout = a.wout + (size_t)b * tw * N;
+    bool finite = isfinite(a.c) && isfinite(a.tau);
+    for (int i = 0; i < N; ++i) finite = finite && isfinite(wp[i]);
+    for (int k = 0; k < H * N; ++k) finite = finite && isfinite(y[k]);
+    if (!finite) {
+        for (int t = 0; t < tw; ++t)
+            for (int i = 0; i < N; ++i) wout[(size_t)t * N + i] = wp[i];   // mpc.py:113-115
+        a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+        a.obj[b] = __builtin_nan("");
+        if (a.iters) a.iters[b] = 0;
+        return;
+    }
+    double f = 0.0;
+    int pcnt = 0;   // the previous period's face (its weights for the L1 term)
+    float pym = 0.0f;
+    for (int t = 0; t < H; ++t) {
+        const float* yt = y + (size_t)t * N;
+        float ym = yt[0];
+        for (int i = 1; i < N; ++i) ym = fmaxf(ym, yt[i]);
+        int cnt = 0;
+        for (int i = 0; i < N; ++i) cnt += yt[i] == ym;
+        const double w = 1.0 / cnt;
+        double rw = 0.0, l1 = 0.0;
+        for (int i = 0; i < N; ++i) {
+            const bool on = yt[i] == ym;
+            const double wi = on ? w : 0.0;
+            rw += (1.0 + expm1((double)yt[i])) * wi;
+            const double wprev = t == 0 ? wp[i] : ((y[(size_t)(t - 1) * N + i] == pym) ? 1.0 / pcnt : 0.0);
+            l1 += fabs(wi - wprev);
+            if (t < tw) wout[(size_t)t * N + i] = wi;
+        }
+        f += log(rw) - a.c * l1;
+        pcnt = cnt;
+        pym = ym;
+    }
+    a.status[b] = KMPC_STATUS_OPTIMAL;
+    a.obj[b] = f;
+    if (a.iters) a.iters[b] = 0;
+}
 
 SolveArgs make_args(const kmpc_solve_desc* d) {
     SolveArgs a;
@@ -47,6 +106,7 @@ bool use_big(const SolveArgs& a) {
 size_t solve_workspace_bytes(const kmpc_solve_desc* d) {
     if (!d || d->B <= 0) return 0;
     const SolveArgs a = make_args(d);
+    if (simplex_case(a)) return 0;
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_ws_bytes(a);
 #endif
@@ -60,6 +120,10 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
+    if (simplex_case(a)) {
+        hipLaunchKernelGGL(simplex_kernel, dim3((a.B + 63) / 64), dim3(64), 0, stream, a);
+        return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+    }
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_launch(a, ws, ws_bytes, stream);
 #endif

@@ -120,3 +120,43 @@ def test_full_size_properties_and_determinism():
     assert turn.max() <= 0.2 + 1e-8
     hold = np.log(np.exp(y.astype(np.float64)) @ wp[:, :, None])[..., 0].sum(-1)
     assert (val >= hold - 1e-9).all()
+
+
+def test_simplex_presolve_matches_ipm_and_oracle():
+    """c = tau = 0, no short (BASELINE configs[1]): the closed-form presolve returns the IPM's
+    optimum — the argmax vertex per period, the centre of the face on exact ties."""
+    import ctypes
+    from koopman_mpc_portfolio_rebalancing_amd import _lib
+    rng = np.random.default_rng(5)
+    B, N, H = 64, 30, 5
+    wp = rng.dirichlet(np.ones(N), B)
+    y = rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32)
+    y[0, 1, [3, 7]] = y[0, 1].max() + 0.01          # an exact two-way tie
+    y[1, :, :] = 0.0                                 # flat window: every asset tied
+    W, st, val = _solve(wp, y, 0.0, 0.0)
+    assert (st == 0).all()
+    am = y.argmax(-1)
+    for b in range(2, B):
+        assert np.array_equal(W[b], np.eye(N)[am[b]])
+    assert np.array_equal(W[0, 1, [3, 7]], [0.5, 0.5]) and W[0, 1].sum() == 1.0
+    assert np.allclose(W[1], 1.0 / N, rtol=0, atol=1e-15)
+    for b in range(4):
+        assert val[b] == pytest.approx(dense_ipm.reference_objective(W[b], wp[b], y[b], 0.0), abs=1e-12)
+    # the interior-point kernels (debug path 1) reach the same optimum
+    L = _lib.load()
+    L.kmpc_debug_solver_path.argtypes = [ctypes.c_int]
+    old = L.kmpc_debug_solver_path(1)
+    try:
+        Wi, sti, vali = _solve(wp, y, 0.0, 0.0)
+    finally:
+        L.kmpc_debug_solver_path(old)
+    assert (sti == 0).all()
+    # exact vs interior point stopped at mu 1e-9 (scaled): never worse, within the parity bar
+    assert (val >= vali - 1e-12).all() and np.abs(val - vali).max() < 1e-7
+    assert np.abs(W[2:] - Wi[2:]).max() < 1e-3        # (near-ties keep the IPM iterate ~1e-5 inside)
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y, 0.0, 0.0)
+    assert (val >= valo - 1e-12).all() and np.abs(val - valo).max() < 1e-8
+    # non-finite input: solver_error with the reference fallback
+    y2 = y[:2].copy(); y2[1, 0, 0] = np.nan
+    W2, st2, val2 = _solve(wp[:2], y2, 0.0, 0.0)
+    assert st2.tolist() == [0, 4] and np.isnan(val2[1]) and np.array_equal(W2[1], np.tile(wp[1], (H, 1)))
