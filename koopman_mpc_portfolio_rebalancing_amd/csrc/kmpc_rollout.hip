@@ -294,6 +294,128 @@ __global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
     }
 }
 
+// Fused latent steps (fp32, single-layer decoder): the whole H-step loop of backtest.py:101-119
+// in one launch. A block owns 32 windows; their z rows stay in LDS for all H steps (ping-pong
+// tiles), each step computes z <- z K on v_mfma_f32_32x32x2_f32 (K^T rows streamed from L2, the
+// next 32-k chunk prefetched under the current one), the ball norm if any (model.py:750-751),
+// then decode rows 0..N-1 with bias + de-standardize straight into yhat[:, k, :]
+// (model.py:768-777, data_finance.py:729-742). Same k order per MFMA lane as gemm_nt_kernel (lane
+// (r, h) consumes k = k0 + 16 h + s); the chunks alternate between two accumulators, so the
+// fp32 sums are regrouped (not bit-identical to the unfused launches; within the rollout tests'
+// 1e-4 of the reference). Replaces 2H small GEMM launches that are latency-bound at small batch.
+struct LatentArgs {
+    int B, L, N, H;
+    const float* z0;     // [B, L]
+    const float* Kt;     // [L, L]: row j = column j of K
+    const float* D;      // decoder rows 0..N-1, [N, L]
+    const float* bias;   // [N] or null
+    const float* mean; const float* stdv;
+    float* yhat;         // [B, H, N]
+    int ball;
+};
+constexpr int LAT_ROWS = 32;
+
+// acc (+)= A[32 rows of As, stride lda] . B[32 rows of Bg, stride L]^T over k in [0, L)
+__device__ __forceinline__ void tile_dot(const float* As, int lda, const float* Bg, int L, bool brow_ok,
+                                         int lane, f32x16& acc) {
+    const int r = lane & 31, h = lane >> 5;
+    f32x16 acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc1[i] = 0.0f;
+    const float* pa = As + r * lda + 16 * h;
+    const float* pb = Bg + (size_t)r * L + 16 * h;
+    f32x4 bn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bn[q] = brow_ok ? *(const f32x4*)(pb + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < L; k0 += 32) {
+        float af[16], bf[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 x = *(const f32x4*)(pa + k0 + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { af[4 * q + e] = x[e]; bf[4 * q + e] = bn[q][e]; }
+        }
+        if (k0 + 32 < L) {   // next chunk of B under this chunk's MFMAs
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bn[q] = brow_ok ? *(const f32x4*)(pb + k0 + 32 + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if ((k0 >> 5) & 1) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc1, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += acc1[i];
+}
+
+__global__ void __launch_bounds__(256) latent_steps_kernel(LatentArgs a) {
+    extern __shared__ float zs[];   // [2][32][L + 4]
+    const int L = a.L, LS = L + 4, N = a.N;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
+    const int m0 = blockIdx.x * LAT_ROWS;
+    float* zc = zs;
+    float* zn = zs + LAT_ROWS * LS;
+    for (int idx = tid; idx < LAT_ROWS * L; idx += 256) {
+        const int row = idx / L, col = idx - row * L;
+        zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
+    }
+    __syncthreads();
+    const int nct = L / 32, ndt = (N + 31) / 32;
+    for (int k = 0; k < a.H; ++k) {
+        // z <- z K: output column tiles ct = wv, wv + 4, ...
+        for (int ct = wv; ct < nct; ct += 4) {
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+            tile_dot(zc, LS, a.Kt + (size_t)ct * 32 * L, L, true, lane, acc);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                zn[((i & 3) + 8 * (i >> 2) + 4 * h) * LS + ct * 32 + (lane & 31)] = acc[i];
+        }
+        __syncthreads();
+        if (a.ball) {   // x / ||x||_2 per row: 8 threads per row
+            const int row = tid >> 3, part = tid & 7;
+            float sq = 0.0f;
+            for (int j = part; j < L; j += 8) sq += zn[row * LS + j] * zn[row * LS + j];
+            sq += __shfl_xor(sq, 1, 64);
+            sq += __shfl_xor(sq, 2, 64);
+            sq += __shfl_xor(sq, 4, 64);
+            const float nrm = sqrtf(sq);
+            for (int j = part; j < L; j += 8) zn[row * LS + j] = zn[row * LS + j] / nrm;
+            __syncthreads();
+        }
+        // decode rows 0..N-1 (+ bias), de-standardize into yhat[:, k, :]
+        for (int ct = wv; ct < ndt; ct += 4) {
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+            const int nrow = ct * 32 + (lane & 31);
+            tile_dot(zn, LS, a.D + (size_t)ct * 32 * L, L, nrow < N, lane, acc);
+            if (nrow < N) {
+                const float bias = a.bias ? a.bias[nrow] : 0.0f, mu = a.mean[nrow], sd = a.stdv[nrow];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (m < a.B) a.yhat[((size_t)m * a.H + k) * N + nrow] = destandardize(acc[i] + bias, sd, mu);
+                }
+            }
+        }
+        float* t = zc; zc = zn; zn = t;
+        __syncthreads();
+    }
+}
+
+// debug switch (tools / tests only): 0 runs the H-step loop as separate GEMM launches
+static int g_fused = 1;
+
+static bool latent_fusable(const kmpc_rollout_desc* d) {
+    return d->dtype == KMPC_DTYPE_F32 && d->decoder.n_layers == 1 && d->L % 32 == 0 && d->L <= 512 &&
+           !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn != KMPC_NORM_ID && d->norm_fn != KMPC_NORM_BALL);
+}
+
 static int gemm(const GemmArgs& g, hipStream_t s) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
@@ -427,6 +549,15 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
 
     // ---- H x (step_latent, decode[:N], destandardize) ----
+    if (g_fused && latent_fusable(d)) {
+        LatentArgs la;
+        la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
+        la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
+        la.ball = d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL;
+        const size_t lds = sizeof(float) * 2 * LAT_ROWS * (L + 4);
+        hipLaunchKernelGGL(latent_steps_kernel, dim3((Bn + LAT_ROWS - 1) / LAT_ROWS), dim3(256), lds, s, la);
+        return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+    }
     float* zc = z0;
     float* zn = z1;
     for (int k = 0; k < H; ++k) {
@@ -463,3 +594,9 @@ int standardize_launch(int T, int N, const double* y, const double* mean, const 
 }
 
 }  // namespace kmpc
+
+extern "C" int kmpc_debug_rollout_fused(int on) {
+    const int old = kmpc::g_fused;
+    kmpc::g_fused = on;
+    return old;
+}

@@ -27,52 +27,71 @@ bool simplex_case(const SolveArgs& a) {
 // simplex exactly on the face of the assets with the largest yhat_t; the returned point is that
 // face's centre (equal weights over exact ties: the analytic centre an interior-point method
 // converges to, and the vertex e_argmax otherwise). problem.value as the IPM kernels report it
-// (mpc.py:103): sum_t log(R_t . w_t) - c sum_t ||w_t - w_{t-1}||_1 (c <= 0 here). One thread per
-// window: O(H N) loads and no iteration. Non-finite inputs -> solver_error and tile(w_prev).
-__global__ void __launch_bounds__(64) simplex_kernel(SolveArgs a) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.B) return;
+// (mpc.py:103): sum_t log(R_t . w_t) - c sum_t ||w_t - w_{t-1}||_1 (c <= 0 here). One wave per
+// window, lanes over the assets (coalesced loads, wave butterflies for max / tie count / sums).
+// Non-finite inputs -> solver_error and tile(w_prev).
+__device__ __forceinline__ float wmaxf(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wsum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ int wsumi(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+constexpr int SIMPLEX_WAVES = 4;   // windows per 256-thread block
+__global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6);
+    if (b >= a.B) return;   // (whole waves)
     const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
     const float* y = a.yhat + (size_t)b * H * N;
     const double* wp = a.wp + (size_t)b * N;
     double* wout = a.wout + (size_t)b * tw * N;
-    bool finite = isfinite(a.c) && isfinite(a.tau);
-    for (int i = 0; i < N; ++i) finite = finite && isfinite(wp[i]);
-    for (int k = 0; k < H * N; ++k) finite = finite && isfinite(y[k]);
-    if (!finite) {
-        for (int t = 0; t < tw; ++t)
-            for (int i = 0; i < N; ++i) wout[(size_t)t * N + i] = wp[i];   // mpc.py:113-115
-        a.status[b] = KMPC_STATUS_SOLVER_ERROR;
-        a.obj[b] = __builtin_nan("");
-        if (a.iters) a.iters[b] = 0;
+    int bad = !(isfinite(a.c) && isfinite(a.tau));
+    for (int i = lane; i < N; i += 64) bad |= !isfinite(wp[i]);
+    for (int k = lane; k < H * N; k += 64) bad |= !isfinite(y[k]);
+    if (wsumi(bad)) {
+        for (int k = lane; k < tw * N; k += 64) wout[k] = wp[k % N];   // mpc.py:113-115
+        if (lane == 0) {
+            a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+            a.obj[b] = __builtin_nan("");
+            if (a.iters) a.iters[b] = 0;
+        }
         return;
     }
     double f = 0.0;
-    int pcnt = 0;   // the previous period's face (its weights for the L1 term)
     float pym = 0.0f;
+    double pw = 0.0;   // the previous period's face weight
     for (int t = 0; t < H; ++t) {
         const float* yt = y + (size_t)t * N;
-        float ym = yt[0];
-        for (int i = 1; i < N; ++i) ym = fmaxf(ym, yt[i]);
+        float ym = -INFINITY;
+        for (int i = lane; i < N; i += 64) ym = fmaxf(ym, yt[i]);
+        ym = wmaxf(ym);
         int cnt = 0;
-        for (int i = 0; i < N; ++i) cnt += yt[i] == ym;
+        for (int i = lane; i < N; i += 64) cnt += yt[i] == ym;
+        cnt = wsumi(cnt);
         const double w = 1.0 / cnt;
         double rw = 0.0, l1 = 0.0;
-        for (int i = 0; i < N; ++i) {
-            const bool on = yt[i] == ym;
-            const double wi = on ? w : 0.0;
+        for (int i = lane; i < N; i += 64) {
+            const double wi = yt[i] == ym ? w : 0.0;
             rw += (1.0 + expm1((double)yt[i])) * wi;
-            const double wprev = t == 0 ? wp[i] : ((y[(size_t)(t - 1) * N + i] == pym) ? 1.0 / pcnt : 0.0);
+            const double wprev = t == 0 ? wp[i] : (y[(size_t)(t - 1) * N + i] == pym ? pw : 0.0);
             l1 += fabs(wi - wprev);
             if (t < tw) wout[(size_t)t * N + i] = wi;
         }
-        f += log(rw) - a.c * l1;
-        pcnt = cnt;
+        f += log(wsum(rw)) - a.c * wsum(l1);
         pym = ym;
+        pw = w;
     }
-    a.status[b] = KMPC_STATUS_OPTIMAL;
-    a.obj[b] = f;
-    if (a.iters) a.iters[b] = 0;
+    if (lane == 0) {
+        a.status[b] = KMPC_STATUS_OPTIMAL;
+        a.obj[b] = f;
+        if (a.iters) a.iters[b] = 0;
+    }
 }
 
 SolveArgs make_args(const kmpc_solve_desc* d) {
@@ -121,7 +140,8 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
     if (simplex_case(a)) {
-        hipLaunchKernelGGL(simplex_kernel, dim3((a.B + 63) / 64), dim3(64), 0, stream, a);
+        hipLaunchKernelGGL(simplex_kernel, dim3((a.B + SIMPLEX_WAVES - 1) / SIMPLEX_WAVES), dim3(64 * SIMPLEX_WAVES), 0,
+                           stream, a);
         return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
     }
 #ifndef KMPC_DEV_ONLY_H10
