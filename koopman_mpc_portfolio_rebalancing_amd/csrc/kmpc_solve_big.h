@@ -712,13 +712,17 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine) {
     __syncthreads();
 }
 
-// Largest step for the current direction (before the fraction-to-boundary)
+// Largest step for the current direction (before the fraction-to-boundary), and the coefficients
+// c1, c2 of the asset complementarity along it, sum (x + a dx)(l + a dl) = c0 + a c1 + a^2 c2
+// (c0: ph_factor's mu sum) — the Mehrotra centring then needs no sweep of its own (ipm_kernel
+// max_step does the same).
 template <int HM, int FL>
-__device__ __forceinline__ double ph_step(Win<HM, FL>& W) {
+__device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2) {
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
     double a = 1e300, wprev = W.wpi, dwp = 0.0;
+    c1 = c2 = 0.0;
     for (int t = 0; t < H; ++t) {
         double mdw = 0.0;
         if (W.act) {
@@ -728,57 +732,39 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W) {
             dwp = dw;
             double dl1, dl2, dl3;
             W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
-            if (hw) { a = to_bound(e.w, dw, a); a = to_bound(e.l1, dl1, a); }
+            if (hw) {
+                a = to_bound(e.w, dw, a); a = to_bound(e.l1, dl1, a);
+                c1 += e.w * dl1 + e.l1 * dw;
+                c2 += dw * dl1;
+            }
             if (hs) {
-                a = to_bound(e.s - e.d, ds - dd, a);
-                a = to_bound(e.s + e.d, ds + dd, a);
+                const double x2 = e.s - e.d, dx2 = ds - dd, x3 = e.s + e.d, dx3 = ds + dd;
+                a = to_bound(x2, dx2, a);
+                a = to_bound(x3, dx3, a);
                 a = to_bound(e.l2, dl2, a);
                 a = to_bound(e.l3, dl3, a);
+                c1 += x2 * dl2 + e.l2 * dx2 + x3 * dl3 + e.l3 * dx3;
+                c2 += dx2 * dl2 + dx3 * dl3;
             }
             mdw = e.m * dw;
         }
         W.slot(t, mdw);
     }
+    W.slot(H, c1);
+    W.slot(H + 1, c2);
     {
         double z = 0.0, na = -a;
         W.sum_max(z, na);
         a = -na;
     }
-    W.finish(H);
+    W.finish(H + 2);
+    c1 = sh.tot[H];
+    c2 = sh.tot[H + 1];
     for (int t = 0; t < H; ++t) {
         a = to_bound(sh.den[t], sh.tot[t], a);
         if (ht) { a = to_bound(sh.z4[t], sh.dz4[t], a); a = to_bound(sh.l4[t], sh.dl4[t], a); }
     }
     return a;
-}
-
-template <int HM, int FL>
-__device__ __forceinline__ double ph_comp(Win<HM, FL>& W, double a) {
-    auto& sh = W.sh;
-    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
-    const int H = W.H;
-    double acc = 0.0;
-    if (W.act) {
-        double wprev = W.wpi, dwp = 0.0;
-        for (int t = 0; t < H; ++t) {
-            const St e = W.st(t, wprev);
-            wprev = e.w;
-            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
-            dwp = dw;
-            double dl1, dl2, dl3;
-            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
-            if (hw) acc += (e.w + a * dw) * (e.l1 + a * dl1);
-            if (hs) {
-                acc += (e.s - e.d + a * (ds - dd)) * (e.l2 + a * dl2);
-                acc += (e.s + e.d + a * (ds + dd)) * (e.l3 + a * dl3);
-            }
-        }
-    }
-    double z = 0.0;
-    W.sum_max(acc, z);
-    if (ht)
-        for (int t = 0; t < H; ++t) acc += (sh.z4[t] + a * sh.dz4[t]) * (sh.l4[t] + a * sh.dl4[t]);
-    return acc;
 }
 
 // corrector targets: rc += dz_aff dl_aff - sigma mu (rc4 by its owner)
@@ -881,10 +867,14 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         double step = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
             ph_newton(W, (pass == 0 || mu > REFINE_MU) ? 0 : a.n_refine);
-            const double amax = ph_step(W);
+            double cc1, cc2;
+            const double amax = ph_step(W, cc1, cc2);
             if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
             const double ap = fmin(1.0, amax);
-            double sg = ph_comp(W, ap) * inv_ncon / mu;
+            double comp = mu_l + ap * (cc1 + ap * cc2);
+            if (W.ht())
+                for (int t = 0; t < H; ++t) comp += (sh.z4[t] + ap * sh.dz4[t]) * (sh.l4[t] + ap * sh.dl4[t]);
+            double sg = comp * inv_ncon / mu;
             sg = sg * sg * sg;
             ph_corr(W, sg * mu);
         }

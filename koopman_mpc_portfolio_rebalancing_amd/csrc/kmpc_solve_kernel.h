@@ -561,38 +561,44 @@ struct Reducer {
             out[2] = o[0]; out[3] = o[1];
         }
     }
-    // per-period sums of a (in place) and the block minimum of mn, sharing one barrier
-    __device__ __forceinline__ double periods_min(double (&a)[HM], double mn) {
-        constexpr int M = pow2_at_least(HM);
+    // per-period sums of a (in place), the block minimum of mn and the block sums of two scalars
+    // (slots HM, HM + 1 of the same reduce-scatter), sharing one barrier
+    __device__ __forceinline__ double periods_min_sums(double (&a)[HM], double mn, double& s1, double& s2) {
+        constexpr int M = pow2_at_least(HM + 2);
         constexpr int RW = Shared<HM, NWM>::RW;
         static_assert(RW > M, "a spare reduction slot per wave");
         const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
         double v[M];
 #pragma unroll
-        for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : 0.0;
+        for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : (t == HM ? s1 : (t == HM + 1 ? s2 : 0.0));
         const int slot = wave_reduce_scatter<M>(v);
         mn = wave_min(mn);
         double* r = &sh.red[buf][0][0];
         if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
         if (lane == 0) r[wv * RW + M] = mn;
         __syncthreads();
-        double t0[NWM][HM + 1];
+        double t0[NWM][HM + 3];
 #pragma unroll
         for (int q = 0; q < NWM; ++q)
 #pragma unroll
-            for (int j = 0; j <= HM; ++j) t0[q][j] = (q == 0 || q < nw) ? r[q * RW + (j < HM ? j : M)] : 0.0;
+            for (int j = 0; j <= HM + 2; ++j) t0[q][j] = (q == 0 || q < nw) ? r[q * RW + (j <= HM + 1 ? j : M)] : 0.0;
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < HM; ++j) {
-            double s = t0[0][j];
+            double sm = t0[0][j];
 #pragma unroll
-            for (int q = 1; q < NWM; ++q) s += t0[q][j];
-            a[j] = s;
+            for (int q = 1; q < NWM; ++q) sm += t0[q][j];
+            a[j] = sm;
         }
-        double m = t0[0][HM];
+        s1 = t0[0][HM];
+        s2 = t0[0][HM + 1];
+        double m = t0[0][HM + 2];
 #pragma unroll
-        for (int q = 1; q < NWM; ++q)
-            if (q < nw) m = fmin(m, t0[q][HM]);
+        for (int q = 1; q < NWM; ++q) {
+            s1 += t0[q][HM];
+            s2 += t0[q][HM + 1];
+            if (q < nw) m = fmin(m, t0[q][HM + 2]);
+        }
         buf ^= Shared<HM, NWM>::NB - 1;
         return m;
     }
@@ -941,11 +947,16 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     KMPC_PH(np, 15);
 }
 
-// Largest step for the current direction (before the caller's fraction-to-boundary).
+// Largest step for the current direction (before the caller's fraction-to-boundary), and the
+// coefficients of the asset complementarity along it, sum_i,t (x + a dx)(l + a dl) =
+// c0 + a c1 + a^2 c2 (c0 is the residual phase's mu sum): block-summed in spare slots of the same
+// reduction, so the Mehrotra centring needs no pass or barrier of its own.
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R) {
+__device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+                                           double& c1, double& c2) {
     const int H = T.H;
     double a = 1e300, mdw[HM];
+    c1 = c2 = 0.0;
     double DL1[HM], DL2[HM], DL3[HM];
     T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
@@ -955,17 +966,24 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
             const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
             const double d = T.w[t] - T.wprev(t);
             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
-            if (T.hw) { a = to_bound(T.w[t], T.dw[t], a); a = to_bound(T.l1[t], dl1, a); }
+            if (T.hw) {
+                a = to_bound(T.w[t], T.dw[t], a); a = to_bound(T.l1[t], dl1, a);
+                c1 += T.w[t] * dl1 + T.l1[t] * T.dw[t];
+                c2 += T.dw[t] * dl1;
+            }
             if (T.hs) {
-                a = to_bound(T.s[t] - d, T.ds[t] - dd, a);
-                a = to_bound(T.s[t] + d, T.ds[t] + dd, a);
+                const double x2 = T.s[t] - d, dx2 = T.ds[t] - dd, x3 = T.s[t] + d, dx3 = T.ds[t] + dd;
+                a = to_bound(x2, dx2, a);
+                a = to_bound(x3, dx3, a);
                 a = to_bound(T.l2[t], dl2, a);
                 a = to_bound(T.l3[t], dl3, a);
+                c1 += x2 * dl2 + T.l2[t] * dx2 + x3 * dl3 + T.l3[t] * dx3;
+                c2 += dx2 * dl2 + dx3 * dl3;
             }
             mdw[t] = T.m[t] * T.dw[t];
         }
     }
-    a = R.periods_min(mdw, a);
+    a = R.periods_min_sums(mdw, a, c1, c2);
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         if (t < H) {
@@ -974,32 +992,6 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
         }
     }
     return a;
-}
-
-template <int HM, int NWM, class TH>
-__device__ __forceinline__ double complementarity(const TH& T, Shared<HM, NWM>& sh,
-                                                  Reducer<HM, NWM>& R, double a) {
-    const int H = T.H;
-    double acc = 0.0;
-    double DL1[HM], DL2[HM], DL3[HM];
-    T.dual_dirs_all(DL1, DL2, DL3);
-#pragma unroll
-    for (int t = 0; t < HM; ++t) {
-        if (T.act && t < H) {
-            const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
-            const double d = T.w[t] - T.wprev(t);
-            const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
-            if (T.hw) acc += (T.w[t] + a * T.dw[t]) * (T.l1[t] + a * dl1);
-            if (T.hs) {
-                acc += (T.s[t] - d + a * (T.ds[t] - dd)) * (T.l2[t] + a * dl2);
-                acc += (T.s[t] + d + a * (T.ds[t] + dd)) * (T.l3[t] + a * dl3);
-            }
-        }
-    }
-    double r = R.sum1(acc);
-    if (T.ht)
-        for (int t = 0; t < H; ++t) r += (sh.z4[t] + a * sh.dz4[t]) * (sh.l4[t] + a * sh.dl4[t]);
-    return r;
 }
 
 // Factor: slack reciprocals, per-asset LDL^T of Q, the Schur matrix G (one Q^{-1} column per
@@ -1474,6 +1466,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 }
                 double mu;
                 R.sum_max(mu_l, rd, mu, rd);
+                const double mu_assets = mu;   // c0 of the complementarity polynomial (max_step)
                 double pr = 0.0;
                 bool domain_ok = true;
                 for (int t = 0; t < H; ++t) {
@@ -1529,10 +1522,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     // (before that G is well conditioned and the IPM self-corrects) — as the oracle
                     newton<HM, NWM>(T, sh, R, (pass == 0 || mu > REFINE_MU) ? 0 : args.n_refine);
                     KMPC_PH(ph, 4);
-                    const double amax = max_step<HM, NWM>(T, sh, R);
+                    double cc1, cc2;
+                    const double amax = max_step<HM, NWM>(T, sh, R, cc1, cc2);
                     if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
                     const double ap = fmin(1.0, amax);
-                    double sg = complementarity<HM, NWM>(T, sh, R, ap) * inv_ncon / mu;
+                    double comp = mu_assets + ap * (cc1 + ap * cc2);
+                    if (T.ht)
+                        for (int t = 0; t < H; ++t) comp += (sh.z4[t] + ap * sh.dz4[t]) * (sh.l4[t] + ap * sh.dl4[t]);
+                    double sg = comp * inv_ncon / mu;
                     sg = sg * sg * sg;
                     const double smu = sg * mu;
                     double DL1[HM], DL2[HM], DL3[HM];
