@@ -114,35 +114,43 @@ __device__ __forceinline__ double to_bound(double v, double dv, double a) {
     return dv < 0.0 ? fmin(a, -v / dv) : a;
 }
 
-// x = M^{-1} b with M = L L' (lower factor in place, row stride np); thread r owns row r.
-__device__ double chol_solve(const double* M, int n, int np, double b, double* vec) {
+// M and its factor L are stored packed lower-triangular, row r at r (r + 1) / 2: the factorization
+// and the solves only touch entries (r, c <= r), and the packed window fits three per CU at n = 100.
+__device__ __forceinline__ size_t tri(int r, int c) { return (size_t)r * (r + 1) / 2 + c; }
+
+// x = M^{-1} b with M = L L' (lower factor in place, packed); thread r owns row r. (A
+// single-wave variant with the vector in registers and v_readlane broadcasts measured no faster at
+// n = 100 and 11% slower at n = 300: the factorization, not the solves, bounds this kernel.)
+__device__ double chol_solve(const double* M, int n, double b, double* vec) {
     const int r = threadIdx.x;
     double x = b;
     for (int j = 0; j < n; ++j) {
-        if (r == j) vec[j] = x / M[j * np + j];
+        if (r == j) vec[j] = x / M[tri(j, j)];
         __syncthreads();
-        if (r > j && r < n) x -= M[r * np + j] * vec[j];
+        if (r > j && r < n) x -= M[tri(r, j)] * vec[j];
     }
     double y = r < n ? vec[r] : 0.0;
     __syncthreads();
     for (int j = n - 1; j >= 0; --j) {
-        if (r == j) vec[j] = y / M[j * np + j];
+        if (r == j) vec[j] = y / M[tri(j, j)];
         __syncthreads();
-        if (r < j) y -= M[j * np + r] * vec[j];
+        if (r < j) y -= M[tri(j, r)] * vec[j];
     }
     const double out = r < n ? vec[r] : 0.0;
     __syncthreads();
     return out;
 }
 
+
 // One window. GM: M and Y in the block's workspace slab (else in LDS after the small arrays).
 template <bool GM>
 __device__ __forceinline__ void mv_window(const MvArgs& a, int b, double* lds) {
-    const int N = a.N, H = a.H, n = N * H, np = n | 1;
+    const int N = a.N, H = a.H, n = N * H;
     double* vec = lds;                      // [n] broadcast vector
     double* Sm = vec + n;                   // [H][H] A M^{-1} A', then its Cholesky factor
-    double* M = GM ? a.ws + (size_t)blockIdx.x * a.slab : Sm + H * H + 4 * H + 18;   // [n][np]: M, then L
-    double* Y = M + (size_t)n * np;         // [H][n] M^{-1} A'
+    double* idg = Sm + H * H + 4 * H + 18;  // [n] 1 / L_jj of the Cholesky factor
+    double* M = GM ? a.ws + (size_t)blockIdx.x * a.slab : idg + n;   // packed lower: M, then L
+    double* Y = M + tri(n, 0);              // [H][n] M^{-1} A'
     double* pv = Sm + H * H;                // [H] period sums (after Sm in LDS, both variants)
     double* nu = pv + H;                    // [H] budget multipliers
     double* dnu = nu + H;                   // [H]
@@ -210,7 +218,17 @@ __device__ __forceinline__ void mv_window(const MvArgs& a, int b, double* lds) {
             wm = prev_period(w, vec, k, n, N, wpi);   // vec holds w afterwards
             double Sw = 0.0;
             if (act)
-                for (int j = 0; j < N; ++j) Sw += Sig[(size_t)i * N + j] * vec[t * N + j];
+            {   // Sigma w per element: column i (= row i, symmetric: coalesced across the block),
+                // four partial sums so the L2 loads of a group are in flight together
+                double s4[4] = {0.0, 0.0, 0.0, 0.0};
+                int j = 0;
+                for (; j + 4 <= N; j += 4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s4[e] += Sig[(size_t)(j + e) * N + i] * vec[t * N + j + e];
+                }
+                for (; j < N; ++j) s4[0] += Sig[(size_t)j * N + i] * vec[t * N + j];
+                Sw = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            }
             const double d = w - wm;
             const double rg2 = (act && hs) ? (s - d) - z2 : 0.0, rg3 = (act && hs) ? (s + d) - z3 : 0.0;
             const double eta = l2 - l3;
@@ -242,37 +260,67 @@ __device__ __forceinline__ void mv_window(const MvArgs& a, int b, double* lds) {
             const double P = (act && hs) ? 1.0 / (al + be) : 0.0;
             const double E = 4.0 * al * be * P;
             const double En = next_period(E, vec, k, n, N);
-            if (act) {
-                for (int l = 0; l < n; ++l) {
+            if (act) {   // column k, rows l >= k (M symmetric): lanes write consecutive entries
+                for (int l = k; l < n; ++l) {
                     const int tl = l / N, j = l - tl * N;
-                    double v = (tl == t) ? g2 * Sig[(size_t)i * N + j] : 0.0;
+                    double v = (tl == t) ? g2 * Sig[(size_t)j * N + i] : 0.0;
                     if (l == k) v += W1 + E + En;
                     if (l == k + N) v -= En;
-                    if (l == k - N) v -= E;
-                    M[(size_t)k * np + l] = v;
+                    M[tri(l, k)] = v;
                 }
             }
             if (k == 0) *flag = 0;
             __syncthreads();
-            for (int j = 0; j < n; ++j) {
-                if (k == j) {
-                    const double dj = M[(size_t)j * np + j];
-                    if (!(dj > 0.0) || !(dj < 1e300)) *flag = 1;
-                    M[(size_t)j * np + j] = sqrt(fmax(dj, 1e-300));
+            // right-looking Cholesky in panels of PB columns (thread k owns row k): inside a panel
+            // column by column (pivot, scale, update of the panel's remaining columns); then the
+            // trailing matrix at once, M[k][c] -= L[k][panel] . L[c][panel] with row k's panel in
+            // registers — one read-modify-write per entry per panel instead of per column
+            constexpr int PB = 8;
+            for (int jb = 0; jb < n; jb += PB) {
+                const int je = jb + PB < n ? jb + PB : n;
+                for (int j = jb; j < je; ++j) {
+                    if (k == j) {
+                        const double dj = M[tri(j, j)];
+                        if (!(dj > 0.0) || !(dj < 1e300)) *flag = 1;
+                        const double lj = sqrt(fmax(dj, 1e-300));
+                        M[tri(j, j)] = lj;
+                        idg[j] = 1.0 / lj;
+                    }
+                    __syncthreads();
+                    if (k > j && k < n) M[tri(k, j)] *= idg[j];
+                    __syncthreads();   // column j of L complete before any row reads it
+                    if (k > j && k < n) {
+                        double* mr = M + tri(k, 0);
+                        const double lkj = mr[j];
+                        const int qe = k < je - 1 ? k : je - 1;   // the panel's columns in row k
+                        for (int q = j + 1; q <= qe; ++q) mr[q] = fma(-lkj, M[tri(q, j)], mr[q]);
+                    }
                 }
                 __syncthreads();
-                if (k > j && k < n) M[(size_t)k * np + j] /= M[(size_t)j * np + j];
-                __syncthreads();
-                if (k > j && k < n) {
-                    const double lkj = M[(size_t)k * np + j];
-                    for (int q = j + 1; q <= k; ++q) M[(size_t)k * np + q] -= lkj * M[(size_t)q * np + j];
+                if (k >= je && k < n) {
+                    double* mr = M + tri(k, 0);
+                    double lk[PB];
+#pragma unroll
+                    for (int p = 0; p < PB; ++p) lk[p] = jb + p < je ? mr[jb + p] : 0.0;
+                    for (int c = je; c <= k; ++c) {
+                        const double* mc = M + tri(c, jb);
+                        double lc[PB];
+#pragma unroll
+                        for (int p = 0; p < PB; ++p) lc[p] = jb + p < je ? mc[p] : 0.0;
+                        double v = mr[c];
+#pragma unroll
+                        for (int p = 0; p < PB; ++p) v = fma(-lk[p], lc[p], v);
+                        mr[c] = v;
+                    }
                 }
+                __syncthreads();
             }
             __syncthreads();
             if (*flag) break;
             // Y = M^{-1} A' (one column per period) and S = A Y
             for (int q = 0; q < H; ++q) {
-                const double yq = chol_solve(M, n, np, (act && t == q) ? 1.0 : 0.0, vec);
+                const double bq = (act && t == q) ? 1.0 : 0.0;
+                const double yq = chol_solve(M, n, bq, vec);
                 if (act) Y[(size_t)q * n + k] = yq;
                 period_sums(yq, vec, pv, k, n, N, H);
                 if (k < H) Sm[k * H + q] = pv[k];
@@ -305,7 +353,7 @@ __device__ __forceinline__ void mv_window(const MvArgs& a, int b, double* lds) {
                 const double v = (act && hs) ? (be - al) * P * qs + p3 - p2 : 0.0;
                 const double vn = next_period(v, vec, k, n, N);
                 const double rhs = act ? -rw - (hw ? rc1 / w : 0.0) - (v - vn) : 0.0;
-                const double x = chol_solve(M, n, np, rhs, vec);
+                const double x = chol_solve(M, n, rhs, vec);
                 period_sums(x, vec, pv, k, n, N, H);
                 if (k == 0) {   // dnu = S^{-1} (A x + r_p)
                     for (int j = 0; j < H; ++j) {
@@ -427,18 +475,18 @@ __global__ void rolling_moments_kernel(int B, int T, int N, int lookback, const 
 
 }  // namespace
 
-// LDS of the small arrays (vec, Sm, pv, nu, dnu, rpv, red, flag) and, for the LDS variant, M and Y
+// LDS of the small arrays (vec, Sm, pv, nu, dnu, rpv, red, flag, idg) and, for the LDS variant, M and Y
 size_t mv_small_bytes(int N, int H) {
-    return sizeof(double) * ((size_t)N * H + (size_t)H * H + 4 * (size_t)H + 18);
+    return sizeof(double) * (2 * (size_t)N * H + (size_t)H * H + 4 * (size_t)H + 18);
 }
 size_t mv_lds_bytes(int N, int H) {
-    const size_t n = (size_t)N * H, np = n | 1;
-    return mv_small_bytes(N, H) + sizeof(double) * (n * np + H * n);
+    const size_t n = (size_t)N * H;
+    return mv_small_bytes(N, H) + sizeof(double) * (n * (n + 1) / 2 + H * n);
 }
 static bool mv_in_lds(int N, int H) { return (size_t)N * H <= 128 && mv_lds_bytes(N, H) <= 160 * 1024; }
 static size_t mv_slab(int N, int H) {
-    const size_t n = (size_t)N * H, np = n | 1;
-    return n * np + H * n;
+    const size_t n = (size_t)N * H;
+    return n * (n + 1) / 2 + H * n;
 }
 size_t mv_workspace_bytes(const kmpc_mv_desc* d) {
     if (!d || d->B <= 0 || mv_in_lds(d->N, d->H)) return 0;

@@ -8,7 +8,7 @@ from koopman_mpc_portfolio_rebalancing_amd.baselines import rolling_moments
 from oracle import mv_ref
 
 dev = torch.device("cuda", 0)
-for N, B in ((20, 65536), (100, 16384)):
+for N, B in ((20, 65536), (100, 16384), (300, 4096)):
     T = 4096
     rng = np.random.default_rng(0)
     z = torch.tensor(rng.normal(0, 1, (T, N)).astype(np.float32), device=dev)
