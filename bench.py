@@ -214,6 +214,63 @@ def secondary_c2(dev, steps: int, warmup: int) -> dict:
             "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
 
 
+def make_lista_state_dict(obs: int, L: int, seed: int = 0) -> dict:
+    """LISTAKM layout (model.py:190-209, 804-850) with LINEAR_ENCODER: the classic LISTA start
+    We = D / Lc, S = I - D D^T / Lc for a random unit-row dictionary D [L, obs], Lc = 1.1 ||D||_2^2
+    (BASELINE configs[4])."""
+    g = torch.Generator().manual_seed(seed)
+    D = torch.randn(L, obs, generator=g)
+    D = D / D.norm(dim=1, keepdim=True)
+    v = torch.randn(obs, generator=g)
+    for _ in range(30):                       # power iteration for ||D||_2
+        v = D.t() @ (D @ v)
+        v = v / v.norm()
+    lc = 1.1 * float((D @ v).norm() ** 2)
+    q, _ = torch.linalg.qr(torch.randn(L, L, generator=g, dtype=torch.float64))
+    sd = {"dict": D, "kmat": (0.95 * q).float(), "dict_init": D.t().contiguous(),
+          "lista.S": torch.eye(L) - (D @ D.t()) / lc, "lista.We.weight": D / lc}
+    return sd, lc
+
+
+def secondary_c5(dev, steps: int, warmup: int, B: int = 1024) -> dict:
+    """BASELINE configs[4] beside the headline: LISTAKM encoder, 500 assets, latent 512, H = 20,
+    bf16 MFMA rollout, the large-window f64 solve (c = 1e-3, tau = 0.2, no short)."""
+    from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
+                                                       solve_mpc_log_utility_batched)
+    N, L, H = 500, 512, 20
+    obs = N * 20
+    sd, lc = make_lista_state_dict(obs, L, seed=2)
+    cfg_m = {"MODEL": {"MODEL_NAME": "LISTAKM", "NORM_FN": "id",
+                       "ENCODER": {"LISTA": {"ALPHA": 5e-3, "L": lc, "NUM_LOOPS": 10}}}}
+    model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, cfg_m), dev, dtype="bf16")
+    mean_d = torch.full((N,), 5e-4, dtype=torch.float32, device=dev)
+    std_d = torch.full((N,), 0.015, dtype=torch.float32, device=dev)
+    x, wp = make_inputs(B, N, obs, seed=200, device=dev)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, allow_short=False)
+    for _ in range(max(warmup, 1)):
+        solve_mpc_log_utility_batched(wp, model.rollout(x, mean_d, std_d, H, N), cfg)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t0 = time.perf_counter()
+    roll, solv = 0.0, 0.0
+    for _ in range(max(steps, 1)):
+        e[0].record()
+        y = model.rollout(x, mean_d, std_d, H, N)
+        e[1].record()
+        W0, st, val = solve_mpc_log_utility_batched(wp, y, cfg)
+        e[2].record()
+        torch.cuda.synchronize()
+        roll += e[0].elapsed_time(e[1])
+        solv += e[1].elapsed_time(e[2])
+    el = time.perf_counter() - t0
+    k = max(steps, 1)
+    return {"workload": f"C5 (BASELINE configs[4]): {B} windows, {N} assets, LISTAKM latent {L} (10 loops, linear "
+                        f"encoder), H={H}, obs {obs}, bf16 MFMA rollout, f64 large-window solve c=1e-3 tau=0.2",
+            "windows_per_s": B * k / el, "ms_per_step": el / k * 1e3, "steps": k,
+            "rollout_ms": roll / k, "solve_ms": solv / k,
+            "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -340,6 +397,7 @@ def main():
         }
         if world == 1:
             line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
+            line["secondary_c5"] = secondary_c5(dev, min(args.steps, 3), min(args.warmup, 1))
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base

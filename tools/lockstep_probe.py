@@ -1,0 +1,32 @@
+"""Dev probe: GPU run_backtest engine (run_backtest_lockstep) throughput —
+P lock-stepped backtest paths of the C3 model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2)
+over T test rows; path-steps/s = P x steps / wall time (one window launch + one bookkeeping
+launch per step)."""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+import bench
+from koopman_mpc_portfolio_rebalancing_amd import (BacktestConfig, DeviceKoopman, KoopmanModelSpec, KoopmanMPCStrategy,
+                                                   MPCConfig)
+from koopman_mpc_portfolio_rebalancing_amd.backtest import run_backtest_lockstep
+
+dev = torch.device("cuda", 0)
+N, L, H = 100, 256, 10
+obs = N * 20
+spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs, L, 1024, seed=0), bench.MODEL_CFG)
+strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+for P, T in ((64, 260), (1024, 260), (8192, 60)):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(P, T, obs, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    cfg = BacktestConfig(horizon=H)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    S = out["return"].shape[1]
+    print(f"P={P} T={T}: {S} steps in {dt*1e3:.1f} ms -> {P*S/dt:.0f} path-steps/s, {dt/S*1e3:.3f} ms/step, "
+          f"final value mean {out['portfolio_value'][:, -1].mean().item():.1f}", flush=True)
