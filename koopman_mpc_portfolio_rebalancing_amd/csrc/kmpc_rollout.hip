@@ -134,31 +134,45 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
 
     const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
                         ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
-        // stage A and B tiles: TM rows x 32 k = 8 TM float4 per operand, TM / 32 per thread
+    // A and B tiles: TM rows x 32 k = 8 TM float4 per operand, TM / 32 per thread. The next
+    // k-tile's global loads are issued into registers before this tile's MFMAs (register double
+    // buffering: one LDS buffer, the HBM / L2 latency under the math).
+    constexpr int QN = TM / 32;
+    f32x4 va[QN], vb[QN];
+    auto fetch = [&](int k0) {
 #pragma unroll
-        for (int q = 0; q < TM / 32; ++q) {
+        for (int q = 0; q < QN; ++q) {
             const int idx = tid + q * 256;          // 0..8 TM - 1
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int kk = k0 + c4;
-            f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+            va[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            vb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
             const int ma = m0 + row, nb = n0 + row;
             if (vec_ok && kk + 3 < g.K) {
-                if (ma < g.M) va = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
-                if (nb < g.N) vb = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
+                if (ma < g.M) va[q] = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
+                if (nb < g.N) vb[q] = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (kk + e < g.K) {
-                        if (ma < g.M) va[e] = g.A[(size_t)ma * g.lda + kk + e];
-                        if (nb < g.N) vb[e] = g.B[(size_t)nb * g.ldb + kk + e];
+                        if (ma < g.M) va[q][e] = g.A[(size_t)ma * g.lda + kk + e];
+                        if (nb < g.N) vb[q][e] = g.B[(size_t)nb * g.ldb + kk + e];
                     }
                 }
             }
-            *(f32x4*)(As + row * LDS_STRIDE + c4) = va;
-            *(f32x4*)(Bs + row * LDS_STRIDE + c4) = vb;
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < g.K; k0 += BK) {
+#pragma unroll
+        for (int q = 0; q < QN; ++q) {
+            const int idx = tid + q * 256;
+            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            *(f32x4*)(As + row * LDS_STRIDE + c4) = va[q];
+            *(f32x4*)(Bs + row * LDS_STRIDE + c4) = vb[q];
         }
         __syncthreads();
+        if (k0 + BK < g.K) fetch(k0 + BK);
         const int r = lane & 31, h = lane >> 5;
         float af[WT][16], bf[WT][16];
 #pragma unroll
