@@ -1635,7 +1635,7 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
     return KMPC_ERR_UNSUPPORTED;
 }
 
-// Constant-case launcher (H == HM, N <= 128): the constraint case is a template argument, so every
+// Constant-case launcher (H == HM, N <= 128; case 7 up to 256): the constraint case is a template argument, so every
 // predicate on it folds away. Cases: 7 = no short + cost + cap (the benchmark's), 1 = no short
 // only (c = tau = 0: the simplex program of BASELINE configs[1]). Returns KMPC_ERR_UNSUPPORTED for
 // any other case (the caller then uses launch_ipm).
@@ -1643,8 +1643,11 @@ template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
     const int nt = WAVE * ((a.N + WAVE - 1) / WAVE);
     const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
-    if (a.H != HM || nt > 128) return KMPC_ERR_UNSUPPORTED;
-    if (fl == 7) return nt <= 64 ? launch_one<HM, 64, true, 7>(a, nt, stream) : launch_one<HM, 128, true, 7>(a, nt, stream);
+    if (a.H != HM || nt > 256) return KMPC_ERR_UNSUPPORTED;
+    if (fl == 7)
+        return nt <= 64 ? launch_one<HM, 64, true, 7>(a, nt, stream)
+                        : (nt <= 128 ? launch_one<HM, 128, true, 7>(a, nt, stream) : launch_one<HM, 256, true, 7>(a, nt, stream));
+    if (nt > 128) return KMPC_ERR_UNSUPPORTED;
     if (fl == 1) return nt <= 64 ? launch_one<HM, 64, true, 1>(a, nt, stream) : launch_one<HM, 128, true, 1>(a, nt, stream);
     return KMPC_ERR_UNSUPPORTED;
 }
