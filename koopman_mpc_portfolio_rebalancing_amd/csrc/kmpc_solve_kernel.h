@@ -832,6 +832,18 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
     KMPC_PH(lp, 11);
 }
 
+// Period owner t: the cap and budget rows of the Newton right-hand side (and the copies the solve
+// reads) from the current rc4, z4 / l4 residuals — written where rc4 changes, before that phase's
+// barrier, so newton() needs no barrier of its own.
+template <int HM, int NWM, class TH>
+__device__ __forceinline__ void newton_rows(const TH& T, Shared<HM, NWM>& sh, int t) {
+    const bool on = t < T.H;
+    sh.b5[t] = (T.ht && on) ? -sh.rc4[t] - sh.l4[t] * sh.rg4[t] : 0.0;
+    sh.b6[t] = on ? -sh.rp[t] : 0.0;
+    sh.lb5[t] = sh.b5[t];
+    sh.lb6[t] = sh.b6[t];
+}
+
 // Full Newton direction for the current rc targets, with adaptive iterative refinement against
 // the unreduced system (one lsolve body for the solve and its refinements).
 // On exit: T.dw, T.ds, sh.dnu, sh.dz4, sh.dl4.
@@ -841,14 +853,8 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     const int H = T.H;
     PhaseClock np;
     KMPC_PH_START(np);
-    if (threadIdx.x < HM) {
-        const int t = threadIdx.x;
-        sh.b5[t] = (T.ht && t < H) ? -sh.rc4[t] - sh.l4[t] * sh.rg4[t] : 0.0;
-        sh.b6[t] = (t < H) ? -sh.rp[t] : 0.0;
-        sh.lb5[t] = sh.b5[t];
-        sh.lb6[t] = sh.b6[t];
-    }
-    __syncthreads();
+    // (the rows b5, b6 and their solve copies lb5, lb6 were written by the period owners behind the
+    // previous barrier: newton_rows)
     double r0[HM], r1[HM];
     double bn = 0.0;   // ||b||_inf of this thread's rows
 #pragma unroll
@@ -1449,6 +1455,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                         sh.rg4[t] = (T.ht && on) ? T.tau - c2 - sh.z4[t] : 0.0;
                         sh.rc4[t] = (T.ht && on) ? sh.z4[t] * sh.l4[t] : 0.0;
                         sh.iz4[t] = 1.0 / sh.z4[t];
+                        newton_rows<HM, NWM>(T, sh, t);   // the predictor's rows
                     }
                     __syncthreads();
                 }
@@ -1550,6 +1557,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                         const int t = threadIdx.x;
                         sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
                     }
+                    if (threadIdx.x < HM) newton_rows<HM, NWM>(T, sh, threadIdx.x);   // the corrector's rows
                     __syncthreads();
                 }
                 if (args.trace && b == 0 && threadIdx.x == 0) args.trace[4 * it + 3] = step;
