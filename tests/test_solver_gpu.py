@@ -161,3 +161,31 @@ def test_simplex_presolve_matches_ipm_and_oracle():
     y2 = y[:2].copy(); y2[1, 0, 0] = np.nan
     W2, st2, val2 = _solve(wp[:2], y2, 0.0, 0.0)
     assert st2.tolist() == [0, 4] and np.isnan(val2[1]) and np.array_equal(W2[1], np.tile(wp[1], (H, 1)))
+
+
+def test_randomized_sweep_of_solver_paths():
+    """Random (N, H, cost, cap, short) draws across every dispatch path — register kernels (64 /
+    128 / 256 threads, constant-case and generic, exact and ragged H), the large-window kernel and
+    the simplex presolve — against the long-double oracle (objective bar of the module docstring;
+    W[0] where the optimum is unique)."""
+    rng = np.random.default_rng(2024)
+    shapes = [(10, 5), (30, 5), (64, 10), (100, 10), (100, 7), (150, 10), (256, 10), (40, 2),
+              (300, 5), (80, 12), (120, 20), (20, 1)]
+    cases = [(1e-3, 0.2, False), (0.0, 0.0, False), (1e-3, 0.0, False), (0.0, 0.3, False),
+             (5e-3, 0.5, True), (1e-3, 0.0, True)]
+    for k, (N, H) in enumerate(shapes):
+        c, tau, short = cases[k % len(cases)]
+        B = 3
+        wp = rng.dirichlet(np.ones(N), B)
+        if short:
+            wp = wp * 1.5 - 0.5 / N
+        y = rng.normal(5e-4, 0.02, (B, H, N)).astype(np.float32)
+        W, st, val = _solve(wp, y, c, tau, short)
+        Wo, sto, valo, _ = oracle.solve_batch(wp, y, c, tau, allow_short=short)
+        assert np.array_equal(st <= 1, sto <= 1), (N, H, c, tau, short, st, sto)
+        ok = sto <= 1
+        assert np.abs(val[ok] - valo[ok]).max() <= 1e-6 + 1e-5 * np.abs(valo[ok]).max(), (N, H, c, tau, short)
+        for b in np.flatnonzero(ok):
+            assert _feasible(W[b], wp[b], tau, short), (N, H, c, tau, short, b)
+        if c > 0 and not short:
+            assert np.abs(W[ok, 0] - Wo[ok, 0]).max() < 1e-3, (N, H, c, tau)
