@@ -59,7 +59,9 @@ extern "C" {
  *          backtest.py:121), w_prev [B, N] float64 (current_weights).
  * Outputs: w_out [B, N] (W[0], what rebalance() applies, backtest.py:131) or [B, H, N] when
  *          return_full_W != 0; status [B]; obj [B] (problem.value, NaN when not optimal);
- *          iters [B] (may be NULL).
+ *          iters [B] (may be NULL; interior-point iterations taken, 0 for windows solved by the
+ *          closed-form presolve: cost_coeff = 0, max_turnover <= 0, no shorting, where the
+ *          program separates into H simplex problems with a vertex optimum).
  * Failure fallback (mpc.py:113-115) is applied in-kernel: w_out = tile(w_prev), obj = NaN.
  * Workspace: kmpc_workspace_bytes(NULL, desc) bytes (0 for windows of N <= 256 assets and
  *          H <= 10 periods, solved in registers; otherwise the large-window kernel keeps each
