@@ -177,24 +177,47 @@ struct Win {
         mx = MX;
         sbuf ^= 1;
     }
+    // block max of a and of b (one barrier)
+    __device__ __forceinline__ void max_max(double& a, double& b) {
+        a = wave_max(a);
+        b = wave_max(b);
+        const int wv = threadIdx.x / WAVE;
+        if ((threadIdx.x & (WAVE - 1)) == 0) { sh.sc[sbuf][wv][0] = a; sh.sc[sbuf][wv][1] = b; }
+        __syncthreads();
+        double A = sh.sc[sbuf][0][0], B = sh.sc[sbuf][0][1];
+        for (int q = 1; q < nw; ++q) { A = fmax(A, sh.sc[sbuf][q][0]); B = fmax(B, sh.sc[sbuf][q][1]); }
+        a = A;
+        b = B;
+        sbuf ^= 1;
+    }
+    // corrector targets of (t, i) from the affine direction: rc + dx dl_aff - smu, written back
+    // (the dl_aff come from the predictor targets still in RC*; ipm_kernel's corrector rows)
+    __device__ __forceinline__ void corr_rc(int t, const St& e, double dw, double ds, double dd, double smu,
+                                            double& r1, double& r2, double& r3) const {
+        const double rc1 = hw() ? at(A_RC1, t) : 0.0;
+        const double rc2 = hs() ? at(A_RC2, t) : 0.0, rc3 = hs() ? at(A_RC3, t) : 0.0;
+        double dl1, dl2, dl3;
+        ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
+        r1 = rc1;
+        r2 = rc2;
+        r3 = rc3;
+        if (hw()) {
+            r1 = rc1 + (dw * dl1 - smu);
+            at(A_RC1, t) = r1;
+        }
+        if (hs()) {
+            r2 = rc2 + ((ds - dd) * dl2 - smu);
+            r3 = rc3 + ((ds + dd) * dl3 - smu);
+            at(A_RC2, t) = r2;
+            at(A_RC3, t) = r3;
+        }
+    }
 };
 
-// (1) period sums R.w, 1'w, 1's -> den, iden, rp, rg4, rc4, iz4, rw (period owners)
+// period owners: den, iden, rp, rg4, rc4, iz4, rw from the slot totals of (R - 1).w, 1'w, 1's
 template <int HM, int FL>
-__device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
+__device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
     auto& sh = W.sh;
-    for (int t = 0; t < W.H; ++t) {
-        double mw = 0.0, w = 0.0, s = 0.0;
-        if (W.act) {
-            w = W.at(A_W, t);
-            mw = W.at(A_M, t) * w;
-            s = W.at(A_S, t);
-        }
-        W.slot(3 * t, mw);
-        W.slot(3 * t + 1, w);
-        W.slot(3 * t + 2, s);
-    }
-    W.finish(3 * W.H);
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
         const bool on = t < W.H;
@@ -209,6 +232,24 @@ __device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
         if (t == 0) sh.flag = 0;
     }
     __syncthreads();
+}
+
+// (1) period sums R.w, 1'w, 1's -> den, iden, rp, rg4, rc4, iz4, rw (period owners)
+template <int HM, int FL>
+__device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
+    for (int t = 0; t < W.H; ++t) {
+        double mw = 0.0, w = 0.0, s = 0.0;
+        if (W.act) {
+            w = W.at(A_W, t);
+            mw = W.at(A_M, t) * w;
+            s = W.at(A_S, t);
+        }
+        W.slot(3 * t, mw);
+        W.slot(3 * t + 1, w);
+        W.slot(3 * t + 2, s);
+    }
+    W.finish(3 * W.H);
+    sums_owner(W);
 }
 
 // (2) dual residual and complementarity sums, per-asset LDL^T of Q (LR, IDD), targets rc (RC*),
@@ -312,15 +353,14 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
     // diagonal of Q^{-1} (dq_t = 1/Dd_t + Lr_{t+1}^2 dq_{t+1}) into X; pi_H for the centring
     int e = 0;
     if (W.act) {
-        double dqn = 0.0, lrn = 0.0;
+        double dqn = 0.0, lrn = 0.0, pi = 1.0;
         for (int t = H - 1; t >= 0; --t) {
             const double dq = W.at(A_IDD, t) + lrn * lrn * dqn;
             W.at(A_X, t) = dq;
             dqn = dq;
             lrn = W.at(A_LR, t);
+            if (t) pi *= fmax(lrn, LR_FLOOR);
         }
-        double pi = 1.0;
-        for (int t = 1; t < H; ++t) pi *= fmax(W.at(A_LR, t), LR_FLOOR);
         frexp(pi, &e);
     }
     const double cen = ldexp(1.0, -(e / 2));
@@ -450,28 +490,44 @@ __device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H) {
 // Newton solve for rhs rows (first: -rdw, -rds with the complementarity targets rc; refinement:
 // the residual arrays R0 / R1, no targets), oracle/kmpc_oracle.c:lsolve. The solution is assigned
 // (first) or added to DW, DS and sh.dnu.
+// corr: the first solve of the corrector — its targets rc + dx_aff dl_aff - smu are formed here
+// from the affine direction (DW, DS) and written back to RC* (no sweep of their own). bn (when
+// non-null): this thread's ||b||_inf over the rows it owns (dual residual and rc targets).
 template <int HM, int FL>
-__device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
+__device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr = false, double smu = 0.0,
+                                          double* bn = nullptr) {
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
     // ---- A: right-hand sides (BW, BS) and px = sum_i P bs ----
     {
         St cur{};
-        double rc2c = 0.0, rc3c = 0.0;
+        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0;
         if (W.act) {
             cur = W.st(0, W.wpi);
-            if (first && hs) { rc2c = W.at(A_RC2, 0); rc3c = W.at(A_RC3, 0); }
+            if (corr) {
+                dwc = W.at(A_DW, 0);
+                W.corr_rc(0, cur, dwc, W.at(A_DS, 0), dwc, smu, rc1c, rc2c, rc3c);
+            } else if (first) {
+                if (hw) rc1c = W.at(A_RC1, 0);
+                if (hs) { rc2c = W.at(A_RC2, 0); rc3c = W.at(A_RC3, 0); }
+            }
         }
         for (int t = 0; t < H; ++t) {
             double px = 0.0;
             if (W.act) {
                 const bool nx = t + 1 < H;
                 St nxt = cur;
-                double rc2n = 0.0, rc3n = 0.0;
+                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0;
                 if (nx) {
                     nxt = W.st(t + 1, cur.w);
-                    if (first && hs) { rc2n = W.at(A_RC2, t + 1); rc3n = W.at(A_RC3, t + 1); }
+                    if (corr) {
+                        dwn = W.at(A_DW, t + 1);
+                        W.corr_rc(t + 1, nxt, dwn, W.at(A_DS, t + 1), dwn - dwc, smu, rc1n, rc2n, rc3n);
+                    } else if (first) {
+                        if (hw) rc1n = W.at(A_RC1, t + 1);
+                        if (hs) { rc2n = W.at(A_RC2, t + 1); rc3n = W.at(A_RC3, t + 1); }
+                    }
                 }
                 double b0, b1, p1 = 0.0, p2 = 0.0, p3 = 0.0, pn = 0.0;
                 if (first) {
@@ -479,12 +535,15 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
                     W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
                     b0 = -rdw;
                     b1 = -rds;
-                    p1 = hw ? -W.at(A_RC1, t) * cur.iw : 0.0;
+                    p1 = hw ? -rc1c * cur.iw : 0.0;
                     if (hs) {
                         p2 = -rc2c * cur.iz2;
                         p3 = -rc3c * cur.iz3;
                         if (nx) pn = -rc3n * nxt.iz3 + rc2n * nxt.iz2;
                     }
+                    if (bn)
+                        *bn = fmax(*bn, fmax(fmax(fabs(rdw), fabs(rds)),
+                                             fmax(fabs(rc1c), fmax(fabs(rc2c), fabs(rc3c)))));
                 } else {
                     b0 = W.at(A_R0, t);
                     b1 = W.at(A_R1, t);
@@ -495,8 +554,10 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
                 W.at(A_BS, t) = bs;
                 px = cur.P * bs;
                 cur = nxt;
+                rc1c = rc1n;
                 rc2c = rc2n;
                 rc3c = rc3n;
+                dwc = dwn;
             }
             W.slot(t, px);
         }
@@ -606,40 +667,29 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first) {
 
 // Newton direction for the current rc targets, adaptive refinement (ipm_kernel newton).
 // On exit: DW, DS, sh.dnu, sh.dz4, sh.dl4.
+// corr: this is the corrector — its targets (rc += dx_aff dl_aff - smu) are formed by the owners
+// (rc4) here and by the first solve's right-hand-side sweep (rc1..rc3).
 template <int HM, int FL>
-__device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine) {
+__device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool corr = false, double smu = 0.0) {
     auto& sh = W.sh;
     const bool hs = W.hs(), ht = W.ht();
     const int H = W.H;
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
+        if (corr && ht && t < H) sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
         sh.b5[t] = (ht && t < H) ? -sh.rc4[t] - sh.l4[t] * sh.rg4[t] : 0.0;
         sh.b6[t] = (t < H) ? -sh.rp[t] : 0.0;
         sh.lb5[t] = sh.b5[t];
         sh.lb6[t] = sh.b6[t];
     }
     __syncthreads();
+    // ||b||_inf of the unreduced system: this thread's rows from the first solve's sweep, the
+    // owner rows here; reduced with the first residual norm
     double bn = 0.0;
-    if (n_refine > 0) {   // ||b||_inf of the unreduced system
-        if (W.act) {
-            St cur = W.st(0, W.wpi);
-            for (int t = 0; t < H; ++t) {
-                const bool nx = t + 1 < H;
-                const St nxt = nx ? W.st(t + 1, cur.w) : cur;
-                double rdw, rds;
-                W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
-                bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
-                                   fmax(fabs(W.at(A_RC1, t)), fmax(fabs(W.at(A_RC2, t)), fabs(W.at(A_RC3, t))))));
-                cur = nxt;
-            }
-        }
-        if (threadIdx.x == 0)
-            for (int t = 0; t < H; ++t) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
-        double z = 0.0;
-        W.sum_max(z, bn);
-    }
+    if (n_refine > 0 && threadIdx.x == 0)
+        for (int t = 0; t < H; ++t) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     for (int r = 0;; ++r) {
-        ph_lsolve(W, r == 0);
+        ph_lsolve(W, r == 0, corr && r == 0, smu, n_refine > 0 && r == 0 ? &bn : nullptr);
         if (r >= n_refine) break;
         // residual of rows (1), (2), (7) of the direction; rows (3)-(6) hold by construction
         for (int t = 0; t < H; ++t) {
@@ -687,10 +737,7 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine) {
         }
         if (threadIdx.x == 0)
             for (int t = 0; t < H; ++t) rn = fmax(rn, fabs(sh.b6[t] - sh.sdw[t]));
-        {
-            double z = 0.0;
-            W.sum_max(z, rn);
-        }
+        W.max_max(rn, bn);   // (bn: block value after the first pass, unchanged by later ones)
         if (rn <= REFINE_RTOL * bn) break;
         if (threadIdx.x < HM) {
             const int t = threadIdx.x;
@@ -767,44 +814,16 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
     return a;
 }
 
-// corrector targets: rc += dz_aff dl_aff - sigma mu (rc4 by its owner)
-template <int HM, int FL>
-__device__ __forceinline__ void ph_corr(Win<HM, FL>& W, double smu) {
-    auto& sh = W.sh;
-    const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
-    const int H = W.H;
-    if (W.act) {
-        double wprev = W.wpi, dwp = 0.0;
-        for (int t = 0; t < H; ++t) {
-            const St e = W.st(t, wprev);
-            wprev = e.w;
-            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
-            dwp = dw;
-            const double rc1 = W.at(A_RC1, t), rc2 = W.at(A_RC2, t), rc3 = W.at(A_RC3, t);
-            double dl1, dl2, dl3;
-            W.ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
-            if (hw) W.at(A_RC1, t) = rc1 + (dw * dl1 - smu);
-            if (hs) {
-                W.at(A_RC2, t) = rc2 + ((ds - dd) * dl2 - smu);
-                W.at(A_RC3, t) = rc3 + ((ds + dd) * dl3 - smu);
-            }
-        }
-    }
-    if (threadIdx.x < HM && ht && (int)threadIdx.x < H) {
-        const int t = threadIdx.x;
-        sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
-    }
-    __syncthreads();
-}
-
-// iterate update (the multiplier directions need the old state: w_{t-1} is carried)
+// iterate update (the multiplier directions need the old state: w_{t-1} is carried), fused with
+// the next iteration's period sums (ph_sums) over the updated w, s
 template <int HM, int FL>
 __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
     auto& sh = W.sh;
     const int H = W.H;
-    if (W.act) {
-        double wprev = W.wpi, dwp = 0.0;
-        for (int t = 0; t < H; ++t) {
+    double wprev = W.wpi, dwp = 0.0;
+    for (int t = 0; t < H; ++t) {
+        double mw = 0.0, wn = 0.0, sn = 0.0;
+        if (W.act) {
             const St e = W.st(t, wprev);
             wprev = e.w;
             const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
@@ -814,18 +833,24 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
             W.at(A_L1, t) = e.l1 + step * dl1;
             W.at(A_L2, t) = e.l2 + step * dl2;
             W.at(A_L3, t) = e.l3 + step * dl3;
-            W.at(A_W, t) = e.w + step * dw;
-            W.at(A_S, t) = e.s + step * ds;
+            wn = e.w + step * dw;
+            sn = e.s + step * ds;
+            W.at(A_W, t) = wn;
+            W.at(A_S, t) = sn;
+            mw = e.m * wn;
         }
+        W.slot(3 * t, mw);
+        W.slot(3 * t + 1, wn);
+        W.slot(3 * t + 2, sn);
     }
-    __syncthreads();   // every ratio test has read z4 / l4 before their owners update them
+    W.finish(3 * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
     if (threadIdx.x < HM && (int)threadIdx.x < H) {
         const int t = threadIdx.x;
         sh.z4[t] += step * sh.dz4[t];
         sh.l4[t] += step * sh.dl4[t];
         sh.nu[t] += step * sh.dnu[t];
     }
-    __syncthreads();
+    sums_owner(W);
 }
 
 template <int HM, int FL>
@@ -835,8 +860,8 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
     const SolveArgs& a = W.a;
     const int H = W.H;
     int it;
+    ph_sums(W);   // later iterations: ph_update's fused sums
     for (it = 0; it < a.max_iter; ++it) {
-        ph_sums(W);
         double mu_l, rd;
         ph_factor(W, mu_l, rd);
         double mu = mu_l, pr = 0.0;
@@ -864,9 +889,9 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         ph_gram(W);
         schur_factor(sh, H, W.ht());
         if (sh.flag) break;
-        double step = 0.0;
+        double step = 0.0, smu = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
-            ph_newton(W, (pass == 0 || mu > REFINE_MU) ? 0 : a.n_refine);
+            ph_newton(W, (pass == 0 || mu > REFINE_MU) ? 0 : a.n_refine, pass == 1, smu);
             double cc1, cc2;
             const double amax = ph_step(W, cc1, cc2);
             if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
@@ -876,7 +901,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
                 for (int t = 0; t < H; ++t) comp += (sh.z4[t] + ap * sh.dz4[t]) * (sh.l4[t] + ap * sh.dl4[t]);
             double sg = comp * inv_ncon / mu;
             sg = sg * sg * sg;
-            ph_corr(W, sg * mu);
+            smu = sg * mu;   // the corrector's targets are formed inside its first solve
         }
         if (a.trace && b == 0 && threadIdx.x == 0) a.trace[4 * it + 3] = step;
         ph_update(W, step);
