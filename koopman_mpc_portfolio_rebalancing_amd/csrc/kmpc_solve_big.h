@@ -41,8 +41,8 @@ constexpr int LDG = 65;            // LDS row stride of G / L (conflict-free row
 constexpr int NWX = 16;            // max waves per window (1024 threads)
 constexpr int MAX_SLOTS = 512;     // windows in flight = workspace slabs
 constexpr double LR_FLOOR = 1e-14;
-#ifndef KMPC_BIG_WPE
-#define KMPC_BIG_WPE 1
+#ifndef KMPC_BIG_WPE   // waves per SIMD of the >= 512-thread kernels: 2 workgroups per CU
+#define KMPC_BIG_WPE 4
 #endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -92,6 +92,24 @@ __device__ __forceinline__ double rcp(double x) {
     return r;
 }
 
+// One slab element of this thread's asset, read and written through the window's buffer
+// descriptor: the lane's byte offset (one VGPR, shared by every array) plus a wave-uniform byte
+// offset per (array, period) — instead of a 64-bit VGPR address per array, which the compiler
+// keeps live across the whole iteration (register pressure that spilled at 2 workgroups per CU).
+struct Ref {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned vo, so;
+    __device__ __forceinline__ operator double() const {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+    }
+    __device__ __forceinline__ const Ref& operator=(double v) const {
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0)), v), rs, vo, so, 0);
+        return *this;
+    }
+    __device__ __forceinline__ const Ref& operator+=(double v) const { return *this = (double)*this + v; }
+};
+
 template <int HM, int FL>
 struct Win {
     const SolveArgs& a;
@@ -102,15 +120,52 @@ struct Win {
     Case<FL> cs;
     double tau, isig, irsig, cs_c, wpi;
     int sbuf;
+    __amdgpu_buffer_rsrc_t rs;   // the slab (wave-uniform base and size)
+    unsigned vo;                 // i * 8
+
+    __device__ __forceinline__ void bind(size_t slab_doubles) {
+        rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, (int)(slab_doubles * sizeof(double)), 0x00020000);
+        vo = (unsigned)i * 8u;
+    }
 
     __device__ __forceinline__ bool hw() const { return cs.hw; }
     __device__ __forceinline__ bool hs() const { return cs.hs; }
     __device__ __forceinline__ bool ht() const { return cs.ht; }
-    __device__ __forceinline__ double& at(int arr, int t) const { return g[((size_t)arr * HM + t) * NP + i]; }
+    __device__ __forceinline__ Ref at(int arr, int t) const { return Ref{rs, vo, (unsigned)((arr * HM + t) * NP) * 8u}; }
     __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
     __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
     __device__ __forceinline__ double wprev(int t) const { return t ? at(A_W, t - 1) : wpi; }
 
+    // the stored state of (t, i) and the direction / targets the step, update and corrector
+    // sweeps read with it: loaded one period ahead of its use, so that a wave keeps the next
+    // period's loads in flight while it computes this one (the sweeps are load-latency bound)
+    struct Pre {
+        double w, s, l1, l2, l3, m, dw, ds, rc1, rc2, rc3, r0, r1;
+    };
+    // dir: + DW, DS; rc: + RC1..RC3; rr: + R0, R1 (a refinement pass's right-hand side)
+    __device__ __forceinline__ Pre pre(int t, bool dir = true, bool rc = true, bool rr = false) const {
+        Pre p{};
+        p.w = at(A_W, t);
+        p.s = at(A_S, t);
+        p.l1 = at(A_L1, t);
+        p.l2 = at(A_L2, t);
+        p.l3 = at(A_L3, t);
+        p.m = at(A_M, t);
+        if (dir) { p.dw = at(A_DW, t); p.ds = at(A_DS, t); }
+        if (rc) { p.rc1 = at(A_RC1, t); p.rc2 = at(A_RC2, t); p.rc3 = at(A_RC3, t); }
+        if (rr) { p.r0 = at(A_R0, t); p.r1 = at(A_R1, t); }
+        return p;
+    }
+    __device__ __forceinline__ St st(const Pre& p, double wp) const {
+        St e;
+        e.w = p.w;
+        e.s = p.s;
+        e.l1 = p.l1;
+        e.l2 = p.l2;
+        e.l3 = p.l3;
+        e.m = p.m;
+        return derive(e, wp);
+    }
     __device__ __forceinline__ St st(int t, double wp) const {
         St e;
         e.w = at(A_W, t);
@@ -119,6 +174,9 @@ struct Win {
         e.l2 = at(A_L2, t);
         e.l3 = at(A_L3, t);
         e.m = at(A_M, t);
+        return derive(e, wp);
+    }
+    __device__ __forceinline__ St derive(St e, double wp) const {
         e.d = e.w - wp;
         e.iw = hw() ? rcp(e.w) : 0.0;
         if (hs()) {
@@ -192,10 +250,11 @@ struct Win {
     }
     // corrector targets of (t, i) from the affine direction: rc + dx dl_aff - smu, written back
     // (the dl_aff come from the predictor targets still in RC*; ipm_kernel's corrector rows)
-    __device__ __forceinline__ void corr_rc(int t, const St& e, double dw, double ds, double dd, double smu,
+    __device__ __forceinline__ void corr_rc(int t, const St& e, const Pre& p, double dd, double smu,
                                             double& r1, double& r2, double& r3) const {
-        const double rc1 = hw() ? at(A_RC1, t) : 0.0;
-        const double rc2 = hs() ? at(A_RC2, t) : 0.0, rc3 = hs() ? at(A_RC3, t) : 0.0;
+        const double dw = p.dw, ds = p.ds;
+        const double rc1 = hw() ? p.rc1 : 0.0;
+        const double rc2 = hs() ? p.rc2 : 0.0, rc3 = hs() ? p.rc3 : 0.0;
         double dl1, dl2, dl3;
         ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
         r1 = rc1;
@@ -501,33 +560,43 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     const int H = W.H;
     // ---- A: right-hand sides (BW, BS) and px = sum_i P bs ----
     {
+        // per period: the raw state, the affine direction (corr), the targets (first) or the
+        // refinement residual (!first)
         St cur{};
-        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0;
+        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0, r0c = 0.0, r1c = 0.0;
         if (W.act) {
-            cur = W.st(0, W.wpi);
+            const auto p = W.pre(0, corr, first, !first);
+            cur = W.st(p, W.wpi);
             if (corr) {
-                dwc = W.at(A_DW, 0);
-                W.corr_rc(0, cur, dwc, W.at(A_DS, 0), dwc, smu, rc1c, rc2c, rc3c);
+                dwc = p.dw;
+                W.corr_rc(0, cur, p, dwc, smu, rc1c, rc2c, rc3c);
             } else if (first) {
-                if (hw) rc1c = W.at(A_RC1, 0);
-                if (hs) { rc2c = W.at(A_RC2, 0); rc3c = W.at(A_RC3, 0); }
+                rc1c = hw ? p.rc1 : 0.0;
+                rc2c = hs ? p.rc2 : 0.0;
+                rc3c = hs ? p.rc3 : 0.0;
             }
+            r0c = p.r0;
+            r1c = p.r1;
         }
         for (int t = 0; t < H; ++t) {
             double px = 0.0;
             if (W.act) {
                 const bool nx = t + 1 < H;
                 St nxt = cur;
-                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0;
+                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0, r0n = 0.0, r1n = 0.0;
                 if (nx) {
-                    nxt = W.st(t + 1, cur.w);
+                    const auto p = W.pre(t + 1, corr, first, !first);
+                    nxt = W.st(p, cur.w);
                     if (corr) {
-                        dwn = W.at(A_DW, t + 1);
-                        W.corr_rc(t + 1, nxt, dwn, W.at(A_DS, t + 1), dwn - dwc, smu, rc1n, rc2n, rc3n);
+                        dwn = p.dw;
+                        W.corr_rc(t + 1, nxt, p, dwn - dwc, smu, rc1n, rc2n, rc3n);
                     } else if (first) {
-                        if (hw) rc1n = W.at(A_RC1, t + 1);
-                        if (hs) { rc2n = W.at(A_RC2, t + 1); rc3n = W.at(A_RC3, t + 1); }
+                        rc1n = hw ? p.rc1 : 0.0;
+                        rc2n = hs ? p.rc2 : 0.0;
+                        rc3n = hs ? p.rc3 : 0.0;
                     }
+                    r0n = p.r0;
+                    r1n = p.r1;
                 }
                 double b0, b1, p1 = 0.0, p2 = 0.0, p3 = 0.0, pn = 0.0;
                 if (first) {
@@ -545,8 +614,8 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                         *bn = fmax(*bn, fmax(fmax(fabs(rdw), fabs(rds)),
                                              fmax(fabs(rc1c), fmax(fabs(rc2c), fabs(rc3c)))));
                 } else {
-                    b0 = W.at(A_R0, t);
-                    b1 = W.at(A_R1, t);
+                    b0 = r0c;
+                    b1 = r1c;
                 }
                 const double bw = b0 + p1 + (p3 - p2) - pn;
                 const double bs = hs ? b1 + p2 + p3 - (ht ? sh.lb5[t] * sh.iz4[t] : 0.0) : 0.0;
@@ -558,6 +627,8 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 rc2c = rc2n;
                 rc3c = rc3n;
                 dwc = dwn;
+                r0c = r0n;
+                r1c = r1n;
             }
             W.slot(t, px);
         }
@@ -770,15 +841,19 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
     const int H = W.H;
     double a = 1e300, wprev = W.wpi, dwp = 0.0;
     c1 = c2 = 0.0;
+    typename Win<HM, FL>::Pre pn{};
+    if (W.act) pn = W.pre(0);
     for (int t = 0; t < H; ++t) {
         double mdw = 0.0;
         if (W.act) {
-            const St e = W.st(t, wprev);
+            const auto p = pn;
+            if (t + 1 < H) pn = W.pre(t + 1);
+            const St e = W.st(p, wprev);
             wprev = e.w;
-            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            const double dw = p.dw, ds = p.ds, dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
-            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+            W.ddirs(e, p.rc1, p.rc2, p.rc3, dw, ds, dd, dl1, dl2, dl3);
             if (hw) {
                 a = to_bound(e.w, dw, a); a = to_bound(e.l1, dl1, a);
                 c1 += e.w * dl1 + e.l1 * dw;
@@ -821,15 +896,19 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
     auto& sh = W.sh;
     const int H = W.H;
     double wprev = W.wpi, dwp = 0.0;
+    typename Win<HM, FL>::Pre pn{};
+    if (W.act) pn = W.pre(0);
     for (int t = 0; t < H; ++t) {
         double mw = 0.0, wn = 0.0, sn = 0.0;
         if (W.act) {
-            const St e = W.st(t, wprev);
+            const auto p = pn;
+            if (t + 1 < H) pn = W.pre(t + 1);
+            const St e = W.st(p, wprev);
             wprev = e.w;
-            const double dw = W.at(A_DW, t), ds = W.at(A_DS, t), dd = dw - dwp;
+            const double dw = p.dw, ds = p.ds, dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
-            W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+            W.ddirs(e, p.rc1, p.rc2, p.rc3, dw, ds, dd, dl1, dl2, dl3);
             W.at(A_L1, t) = e.l1 + step * dl1;
             W.at(A_L2, t) = e.l2 + step * dl2;
             W.at(A_L3, t) = e.l3 + step * dl3;
@@ -910,12 +989,13 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
 }
 
 template <int HM, int MAXT, int FL>
-__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(KMPC_BIG_WPE))) ipm_big(BigArgs A) {
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT >= 512 ? KMPC_BIG_WPE : 1))) ipm_big(BigArgs A) {
     static_assert(3 * HM <= KP - 1, "Schur system must fit one wave");
     __shared__ BigShared<HM> sh;
     const SolveArgs& a = A.s;
     Win<HM, FL> W{a, sh, A.ws + (size_t)blockIdx.x * A.slab, a.N, a.H, A.NP, (int)(blockDim.x / WAVE),
                   (int)threadIdx.x, (int)threadIdx.x < a.N};
+    W.bind(A.slab);
     W.sbuf = 0;
     W.cs.set_case(!a.allow_short, (a.c > 0.0) || (a.tau > 0.0), a.tau > 0.0);
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
