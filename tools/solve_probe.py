@@ -16,4 +16,5 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     torch.cuda.synchronize(); t = time.time()
     W, s, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
     torch.cuda.synchronize(); dt = time.time() - t
-    print(f"{dt*1e3:.1f} ms {B/dt:.0f} win/s iters {it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)}", flush=True)
+    print(f"{dt*1e3:.1f} ms {B/dt:.0f} win/s iters {it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)}"
+          f" sum(obj) {v.double().sum().item():.12e} sum|W0| {W.double().abs().sum().item():.12e}", flush=True)
