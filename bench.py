@@ -365,7 +365,7 @@ def main():
         if f64_rate is not None:
             roof = {"bound": "mfma", "achieved": f64_rate / 1e12, "peak": F64_VALU_PEAK / 1e12,
                     "unit": "TFLOP/s", "frac": f64_rate / F64_VALU_PEAK, "traffic": traffic,
-                    "dtype": "f64", "kernel": "kmpc_solve (ipm_kernel<10,128,true,7>)", "launch_ms": solve_ms,
+                    "dtype": "f64", "kernel": "kmpc_solve (ipm_kernel<10,128,true,7,104,true>)", "launch_ms": solve_ms,
                     "flops": "executed f64 FLOPs per window from PMC (profiles/r02_solve_pmc.json), "
                              "pipe: f64 VALU (no f64 MFMA use; same 78.6 TFLOP/s peak)"}
         else:
