@@ -15,7 +15,7 @@
 // The solve is bound by that HBM / Infinity-Cache stream.
 //
 // Layout: one workgroup per window, one asset per thread (blockDim = 64 ceil(N / 64) <= 1024), a
-// persistent grid of min(B, MAX_SLOTS) workgroups walks the windows (workspace = slots x slab).
+// persistent grid of slots_for(B, N) <= 768 workgroups walks the windows (workspace = slots x slab).
 // Period loops are runtime loops with scalar carries (no per-period register arrays: small code,
 // bounded registers); per-period block sums are wave butterflies (permlane / DPP) per period into
 // LDS slots, then one pass over the waves. Per-period scalars, the Schur matrix and the reduction
@@ -39,7 +39,16 @@ namespace big {
 constexpr int KP = 64;             // padded Schur width (3 HM <= 63)
 constexpr int LDG = 65;            // LDS row stride of G / L (conflict-free row and column reads)
 constexpr int NWX = 16;            // max waves per window (1024 threads)
-constexpr int MAX_SLOTS = 512;     // windows in flight = workspace slabs
+// windows in flight = workspace slabs: two workgroups per CU for the >= 512-thread blocks (the
+// slab stream is HBM-bound there: 768 slots measured -9% at N = 300, H = 15, equal at N = 500),
+// three (the LDS limit) for windows of <= 256 assets, which are latency-bound (N = 100, H = 20:
+// 512 -> 768 slots +17%, measured r02)
+constexpr int MAX_SLOTS = 512;
+constexpr int MAX_SLOTS_SMALL = 768;
+__host__ __device__ inline int slots_for(int B, int N) {
+    const int cap = N <= 256 ? MAX_SLOTS_SMALL : MAX_SLOTS;
+    return B < cap ? B : cap;
+}
 constexpr double LR_FLOOR = 1e-14;
 #ifndef KMPC_BIG_WPE   // waves per SIMD of the >= 512-thread kernels: 2 workgroups per CU
 #define KMPC_BIG_WPE 4
@@ -69,8 +78,8 @@ struct BigShared {
     double G[KP * LDG];          // Schur matrix (lower triangle), then L (unit lower, strictly below)
     double gid[KP];              // 1 / D of G = L D L^T
     double q[KP];                // Schur solution (period-major index 3t + type)
-    double tot[3 * KP];          // block-reduction totals
-    double red[NWX][3 * KP];     // per-wave partial slots of a period reduction
+    double tot[KP];              // block-reduction totals (slots < 3 HM <= 63)
+    double red[NWX][KP];         // per-wave partial slots of a period reduction
     double sc[2][NWX][2];        // per-wave partials of scalar reductions (alternating)
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
@@ -1118,8 +1127,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 template <int HM>
 size_t ws_bytes(const SolveArgs& a) {
     const int NP = WAVE * ((a.N + WAVE - 1) / WAVE);
-    const int slots = a.B < MAX_SLOTS ? a.B : MAX_SLOTS;
-    return sizeof(double) * slab_doubles(HM, NP) * (size_t)slots;
+    return sizeof(double) * slab_doubles(HM, NP) * (size_t)slots_for(a.B, a.N);
 }
 
 template <int HM, int MAXT>
@@ -1138,7 +1146,7 @@ int launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream) {
     A.NP = WAVE * ((a.N + WAVE - 1) / WAVE);
     A.slab = slab_doubles(HM, A.NP);
     A.ws = (double*)ws;
-    const int slots = a.B < MAX_SLOTS ? a.B : MAX_SLOTS;
+    const int slots = slots_for(a.B, a.N);
     const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
     if (A.NP <= 256) return launch_t<HM, 256>(A, slots, stream, fl);
     if (A.NP <= 512) return launch_t<HM, 512>(A, slots, stream, fl);
