@@ -288,7 +288,7 @@ __host__ __device__ constexpr int n_cold(bool ql) { return ql ? 8 : 6; }
 // within one CU's 160 KB; otherwise (HM = 21, or 1024-thread blocks) they stay in registers.
 template <int HM, int MAXT, int CS, bool QL>
 constexpr bool cold_in_lds() {
-    return MAXT <= 256 && (n_cold(QL) * HM * CS + 2 * 9 * HM * HM) * 8 + 16 * 1024 <= 160 * 1024;
+    return MAXT <= 256 && (n_cold(QL) * HM * CS + 9 * HM * HM) * 8 + 16 * 1024 <= 160 * 1024;
 }
 template <int HM, int MAXT, int CS, bool QL>
 constexpr size_t cold_bytes() { return cold_in_lds<HM, MAXT, CS, QL>() ? sizeof(double) * n_cold(QL) * HM * CS : 0; }
@@ -1674,7 +1674,8 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
 // predicate on it folds away. Cases: 7 = no short + cost + cap (the benchmark's), 1 = no short
 // only (c = tau = 0: the simplex program of BASELINE configs[1]). Returns KMPC_ERR_UNSUPPORTED for
 // any other case (the caller then uses launch_ipm).
-constexpr int QL_CS = 104;   // cold-array stride of the QL variant (windows of N < QL_CS assets)
+constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
+constexpr int QL_CS256 = 216;  // ... and of the 256-thread one
 
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
@@ -1685,8 +1686,12 @@ int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
         // N <= 103 at H = 10 (BASELINE configs[2..3]: N = 100): the per-asset LDL^T arrays (iDd, Lr)
         // join the cold arrays in LDS with a 104-lane stride (two windows per CU still fit):
         // 40 VGPRs of live state less, 132 -> 107 spilled dwords, C3 solve +4.5% (measured r02)
-        if constexpr (HM == 10)
+        if constexpr (HM == 10) {
             if (nt == 128 && a.N < QL_CS) return launch_one<HM, 128, true, 7, QL_CS, true>(a, nt, stream);
+            // 256-thread windows (one per CU): the 8 cold arrays at a 216-lane stride fit 160 KB
+            // (151 -> 108 spilled dwords; N = 200 +6.7%, measured r02)
+            if (nt == 256 && a.N < QL_CS256) return launch_one<HM, 256, true, 7, QL_CS256, true>(a, nt, stream);
+        }
         return nt <= 64 ? launch_one<HM, 64, true, 7>(a, nt, stream)
                         : (nt <= 128 ? launch_one<HM, 128, true, 7>(a, nt, stream) : launch_one<HM, 256, true, 7>(a, nt, stream));
     }

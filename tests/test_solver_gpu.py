@@ -89,6 +89,7 @@ def test_fallback_statuses_on_device():
                                  (100, 10), (64, 10),                  # exact-H, constant-case kernel
                                  (65, 10), (103, 10), (104, 10),       # QL variant (N < 104) and its edges
                                  (200, 10), (256, 5),                  # constant-case, 256 threads
+                                 (215, 10), (216, 10),                 # 256-thread QL variant edges
                                  (100, 21), (200, 21), (30, 15),       # HM = 21: exact and ragged H
                                  (500, 20), (700, 3), (520, 10), (1000, 10)])   # 512- and 1024-thread variants
 def test_ragged_shapes_match_oracle(N, H):

@@ -33,6 +33,7 @@ run("C1-shape", 65536, 10, 5, 1e-3, 0.2)
 run("C3", 65536, 100, 10, 1e-3, 0.2)
 run("N=120,H=10", 65536, 120, 10, 1e-3, 0.2)
 run("N=90,H=7", 65536, 90, 7, 1e-3, 0.2)
+run("N=200,H=10", 16384, 200, 10, 1e-3, 0.2)
 run("N=250,H=10", 8192, 250, 10, 1e-3, 0.2)
 run("N=500,H=10", 4096, 500, 10, 1e-3, 0.2)
 run("N=100,H=20", 8192, 100, 20, 1e-3, 0.2)
