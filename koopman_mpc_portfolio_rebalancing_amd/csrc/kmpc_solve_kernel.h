@@ -974,6 +974,9 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
     c1 = c2 = 0.0;
     double DL1[HM], DL2[HM], DL3[HM];
     T.dual_dirs_all(DL1, DL2, DL3);
+    // primal bounds (w, s -+ d) through the slack reciprocals factor() stored for this iterate:
+    // the largest -dx / x, inverted once, instead of one reciprocal per ratio
+    double qx = 0.0;
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         mdw[t] = 0.0;
@@ -982,14 +985,14 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
             const double d = T.w[t] - T.wprev(t);
             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
             if (T.hw) {
-                a = to_bound(T.w[t], T.dw[t], a); a = to_bound(T.l1[t], dl1, a);
+                qx = fmax(qx, -T.dw[t] * T.iw[t]);
+                a = to_bound(T.l1[t], dl1, a);
                 c1 += T.w[t] * dl1 + T.l1[t] * T.dw[t];
                 c2 += T.dw[t] * dl1;
             }
             if (T.hs) {
                 const double x2 = T.s[t] - d, dx2 = T.ds[t] - dd, x3 = T.s[t] + d, dx3 = T.ds[t] + dd;
-                a = to_bound(x2, dx2, a);
-                a = to_bound(x3, dx3, a);
+                qx = fmax(qx, fmax(-dx2 * T.iz2[t], -dx3 * T.iz3[t]));
                 a = to_bound(T.l2[t], dl2, a);
                 a = to_bound(T.l3[t], dl3, a);
                 c1 += x2 * dl2 + T.l2[t] * dx2 + x3 * dl3 + T.l3[t] * dx3;
@@ -998,12 +1001,18 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
             mdw[t] = T.m[t] * T.dw[t];
         }
     }
+    if (qx > 0.0) a = fmin(a, rcp_nr(qx));
+    // the cap slack / multiplier bounds of period t on its owner lane (folded into the block min)
+    if (T.ht && (int)threadIdx.x < H) {
+        const int t = threadIdx.x;
+        a = to_bound(sh.z4[t], sh.dz4[t], a);
+        a = to_bound(sh.l4[t], sh.dl4[t], a);
+    }
     a = R.periods_min_sums(mdw, a, c1, c2);
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         if (t < H) {
             a = to_bound(sh.den[t], mdw[t], a);
-            if (T.ht) { a = to_bound(sh.z4[t], sh.dz4[t], a); a = to_bound(sh.l4[t], sh.dl4[t], a); }
         }
     }
     return a;
