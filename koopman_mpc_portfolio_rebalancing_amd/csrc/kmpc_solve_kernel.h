@@ -1665,6 +1665,9 @@ int launch_one(const SolveArgs& a, int nt, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 
+constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
+constexpr int QL_CS256 = 216;  // ... and of the 256-thread one
+
 // Generic launcher (constraint case read at run time): one workgroup of 64 * ceil(N / 64) threads
 // per window. The 64-thread variant sizes its LDS for one wave, so four one-wave windows share a
 // CU (the 128-thread variant's LDS admits two windows per CU).
@@ -1673,6 +1676,10 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
     const int nt = WAVE * ((a.N + WAVE - 1) / WAVE);
     const bool exact = a.H == HM;
     if (nt <= 64) return exact ? launch_one<HM, 64, true, -1>(a, nt, stream) : launch_one<HM, 64, false, -1>(a, nt, stream);
+    if constexpr (HM == 10)   // QL variant (LDL^T arrays in LDS): 40 -> 0 spilled dwords
+        if (nt == 128 && a.N < QL_CS)
+            return exact ? launch_one<HM, 128, true, -1, QL_CS, true>(a, nt, stream)
+                         : launch_one<HM, 128, false, -1, QL_CS, true>(a, nt, stream);
     if (nt <= 128) return exact ? launch_one<HM, 128, true, -1>(a, nt, stream) : launch_one<HM, 128, false, -1>(a, nt, stream);
     if (nt <= 256) return exact ? launch_one<HM, 256, true, -1>(a, nt, stream) : launch_one<HM, 256, false, -1>(a, nt, stream);
     // past 256 assets a window's state does not fit the registers of one block: kmpc_solve_big.h
@@ -1683,9 +1690,6 @@ int launch_ipm(const SolveArgs& a, hipStream_t stream) {
 // predicate on it folds away. Cases: 7 = no short + cost + cap (the benchmark's), 1 = no short
 // only (c = tau = 0: the simplex program of BASELINE configs[1]). Returns KMPC_ERR_UNSUPPORTED for
 // any other case (the caller then uses launch_ipm).
-constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
-constexpr int QL_CS256 = 216;  // ... and of the 256-thread one
-
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
     const int nt = WAVE * ((a.N + WAVE - 1) / WAVE);

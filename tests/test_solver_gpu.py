@@ -88,6 +88,7 @@ def test_fallback_statuses_on_device():
 @pytest.mark.parametrize("N,H", [(1, 3), (63, 4), (64, 5), (65, 6), (129, 2), (300, 7), (20, 12),
                                  (100, 10), (64, 10),                  # exact-H, constant-case kernel
                                  (65, 10), (103, 10), (104, 10),       # QL variant (N < 104) and its edges
+                                 (100, 9), (103, 7),                   # generic QL variant (ragged H)
                                  (200, 10), (256, 5),                  # constant-case, 256 threads
                                  (215, 10), (216, 10),                 # 256-thread QL variant edges
                                  (100, 21), (200, 21), (30, 15),       # HM = 21: exact and ragged H
