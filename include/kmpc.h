@@ -66,7 +66,8 @@ extern "C" {
  * Workspace: kmpc_workspace_bytes(NULL, desc) bytes (0 for windows of N <= 256 assets and
  *          H <= 10 periods, solved in registers; otherwise the large-window kernel keeps each
  *          window's interior-point state there, ~ (22 H + 128) (64 ceil(N / 64)) doubles per
- *          window for min(B, 512) windows in flight). Too little -> KMPC_ERR_WORKSPACE.
+ *          window for min(B, 768) windows in flight when N <= 256, min(B, 512) otherwise).
+ *          Too little -> KMPC_ERR_WORKSPACE.
  */
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
