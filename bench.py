@@ -13,12 +13,15 @@ inputs resident in HBM before the timed region starts:
 This is the launch sequence kmpc_window issues; it is split here only so that HIP events can
 bracket the solve kernel alone (the dominant kernel) for the roofline figure.
 
-Workload (BASELINE configs[2]): 65536 windows per GPU, N = 100 assets, latent
+Workload. N = 1: BASELINE configs[2], 65536 windows, N = 100 assets, latent
 L = 256, H = 10, obs = N * 20 = 2000, the finance_sparse GenericKM layout (encoder
 Linear(2000,1024)-ReLU-Linear(1024,1024)-ReLU-Linear(1024,256), norm 'id', linear decoder without
-bias), K = random orthogonal x 0.95, MPC cost 1e-3, max_turnover 0.2, no short. Weights and inputs
-are synthetic (seeded), as SURVEY §8d prescribes; multi-GPU is weak scaling (65536 windows per
-rank, rank r draws its own seeded block of the global window stream).
+bias), K = random orthogonal x 0.95, MPC cost 1e-3, max_turnover 0.2, no short. N > 1: BASELINE
+configs[3] (C4), 2^20 windows of the same model per step, rank r taking the contiguous block
+window_range(2^20, N, r) — strong scaling, one RCCL gather of W0 to rank 0. Weights and inputs are
+synthetic and seeded; every window's (obs, w_prev) is a function of its index in ONE global stream
+(window_inputs), so the N = 1 batch is the first 65536 windows of the C4 stream and a window's
+inputs (and result) do not depend on the GPU count.
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch under torch.distributed.run.
 """
@@ -49,7 +52,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--windows", type=int, default=65536, help="windows per GPU per step")
+    p.add_argument("--windows", type=int, default=65536, help="windows per step at N = 1 (configs[2])")
+    p.add_argument("--global-windows", type=int, default=0,
+                   help="windows per step over all ranks (default: --windows at N = 1, 2^20 = configs[3] at N > 1)")
     p.add_argument("--assets", type=int, default=100)
     p.add_argument("--latent", type=int, default=256)
     p.add_argument("--horizon", type=int, default=10)
@@ -91,6 +96,59 @@ def make_inputs(B: int, N: int, obs: int, seed: int, device):
     x = torch.randn(B, obs, generator=g)                                   # standardized embedding
     wp = torch.distributions.Dirichlet(torch.ones(N, dtype=torch.float64)).sample((B,))  # uses global RNG
     return x.to(device), wp.to(device)
+
+
+C4_GLOBAL_WINDOWS = 1 << 20   # BASELINE configs[3]
+STREAM_CHUNK = 4096
+
+
+def window_inputs(lo: int, hi: int, N: int, obs: int, seed: int, device):
+    """Windows [lo, hi) of one global seeded stream: window i's standardized embedding
+    obs_i ~ N(0, 1) and w_prev_i ~ Dirichlet(1_N) (normalised Exp(1) draws) depend only on (seed, i)
+    — each 4096-window chunk c of the stream is drawn from its own generator seeded (seed, c) on
+    `device` — so rank r of N generating window_range(n, N, r) holds exactly those rows of the
+    single-process batch."""
+    g = torch.Generator(device=device)
+    xs, ws = [], []
+    for c in range(lo // STREAM_CHUNK, (hi + STREAM_CHUNK - 1) // STREAM_CHUNK):
+        g.manual_seed(seed * 1_000_003 + c)
+        x = torch.randn(STREAM_CHUNK, obs, generator=g, device=device)
+        e = -torch.log1p(-torch.rand(STREAM_CHUNK, N, generator=g, device=device, dtype=torch.float64))
+        w = e / e.sum(1, keepdim=True)
+        a, b = max(lo, c * STREAM_CHUNK) - c * STREAM_CHUNK, min(hi, (c + 1) * STREAM_CHUNK) - c * STREAM_CHUNK
+        xs.append(x[a:b])
+        ws.append(w[a:b])
+    if not xs:
+        return torch.empty(0, obs, device=device), torch.empty(0, N, dtype=torch.float64, device=device)
+    return torch.cat(xs).contiguous(), torch.cat(ws).contiguous()
+
+
+def timed_loop(step, steps: int, warmup: int, world: int, device):
+    """The bench contract's timing: `warmup` untimed steps, then exactly `steps` steps bracketed by a
+    barrier + device synchronize on both sides; the elapsed time is the MAX over ranks (all_reduce).
+    step(k) runs one step (k = None for warmup) and returns its output; returns (elapsed, last)."""
+    import torch.distributed as dist
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    out = None
+    for _ in range(warmup):
+        out = step(None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        out = step(k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
 
 
 def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg, budget_s):
@@ -149,8 +207,8 @@ def cpu_baseline_serial(sd, mean, std, x_gpu, wp_gpu, H, N, cfg, budget_s):
         K = sd["kmat"]
         D = sd["decoder.network.0.weight"]
         mean_t, std_t = torch.tensor(mean), torch.tensor(std)
-        xs = x_gpu[:256].cpu()
-        wps = wp_gpu[:256].cpu().numpy()
+        xs = x_gpu[:2048].cpu()
+        wps = wp_gpu[:2048].cpu().numpy()
 
         def window(i):
             with torch.no_grad():
@@ -171,7 +229,7 @@ def cpu_baseline_serial(sd, mean, std, x_gpu, wp_gpu, H, N, cfg, budget_s):
         window(0)
         t0 = time.perf_counter()
         n = 0
-        while n < xs.shape[0] and (n < 8 or time.perf_counter() - t0 < budget_s):
+        while n < xs.shape[0] and (n < 1024 or time.perf_counter() - t0 < budget_s):
             window(n)
             n += 1
         dt = time.perf_counter() - t0
@@ -181,6 +239,59 @@ def cpu_baseline_serial(sd, mean, std, x_gpu, wp_gpu, H, N, cfg, budget_s):
             "sample": f"first {n} windows of rank 0's C3 batch, one at a time: torch-CPU batch-1 rollout "
                       f"(backtest.py:99-121 op order, full decode) + float64 C solve (oracle/kmpc_oracle.c), "
                       f"1 thread, {dt:.1f} s"}
+
+
+def cpu_baseline_c1(n_test: int = 1000) -> dict:
+    """BASELINE configs[0]: the reference plumbing on one CPU thread — run_backtest
+    (backtest.py:133-219, restated in oracle/backtest_ref.py) over a synthetic 1000-row test set,
+    10 assets, finance_sparse GenericKM (obs 200, encoder [1024, 1024], latent 128, linear decoder),
+    MPCConfig(horizon=5) / BacktestConfig(horizon=5). Each of the 995 steps runs
+    KoopmanMPCStrategy.rebalance as the reference does: a torch-CPU batch-1 rollout in the op order
+    of backtest.py:99-121 (full obs-width decode, slice, de-standardize per step) and the float64 C
+    solve (oracle/kmpc_oracle.c), then the numpy bookkeeping (cost, realized return, drift)."""
+    from oracle import backtest_ref, solver as osolver
+    N, L, H, emb, hidden = 10, 128, 5, 20, 1024
+    obs = N * emb
+    sd = make_state_dict(obs, L, hidden, seed=10)
+    g = torch.Generator().manual_seed(10)
+    data = torch.randn(n_test, obs, generator=g)                    # standardized embedded test rows
+    mean_t = torch.full((N,), 5e-4)
+    std_t = torch.full((N,), 0.015)
+    all_returns = (data[:, :N] * std_t + mean_t).numpy()            # backtest.py:169-171
+    cfg_m = {"horizon": H, "cost_coeff": 1e-3, "max_turnover": 0.2}
+    enc = [(sd[f"encoder.network.{2 * k}.weight"], sd[f"encoder.network.{2 * k}.bias"]) for k in range(3)]
+    K, D = sd["kmat"], sd["decoder.network.0.weight"]
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+
+    def rebalance(t, w):
+        with torch.no_grad():
+            z = data[t].unsqueeze(0)                                  # backtest.py:85
+            for k, (W, b) in enumerate(enc):
+                z = torch.nn.functional.linear(z, W, b)
+                if k < 2:
+                    z = torch.relu(z)
+            ys = []
+            for _ in range(H):
+                z = z @ K
+                p_ = torch.nn.functional.linear(z, D)
+                ys.append((p_[..., :N] * std_t + mean_t).numpy().flatten())
+        Wm, st, _, _ = osolver.solve(w, np.array(ys), cfg_m["cost_coeff"], cfg_m["max_turnover"], False,
+                                     precision="d")
+        return Wm[0] if st <= 1 else w.copy()
+
+    try:
+        rebalance(0, np.ones(N) / N)
+        t0 = time.perf_counter()
+        hist = backtest_ref.run_backtest(rebalance, all_returns, n_test, H, N, 10000.0, 1, 1e-3)
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(threads)
+    return {"value": len(hist) / dt, "unit": "windows/s", "cores": 1, "kind": "port", "steps": len(hist),
+            "seconds": dt, "final_value": hist[-1]["portfolio_value"],
+            "sample": f"BASELINE configs[0] (C1): full run_backtest, {n_test} synthetic test rows -> {len(hist)} "
+                      f"sequential rebalance steps, 10 assets, latent 128, H=5, obs 200, enc [1024,1024]; torch-CPU "
+                      f"batch-1 rollout + float64 C solve + numpy bookkeeping, 1 thread, {dt:.1f} s"}
 
 
 def secondary_c2(dev, steps: int, warmup: int) -> dict:
@@ -288,8 +399,12 @@ def main():
 
     from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
                                                        solve_mpc_log_utility_batched)
-    from koopman_mpc_portfolio_rebalancing_amd.shard import gather_rows
-    B, N, L, H = args.windows, args.assets, args.latent, args.horizon
+    from koopman_mpc_portfolio_rebalancing_amd.shard import gather_rows, window_range
+    N, L, H = args.assets, args.latent, args.horizon
+    # N = 1: configs[2] (65536 windows); N > 1: configs[3], 2^20 global windows sharded
+    G = args.global_windows or (args.windows if world == 1 else C4_GLOBAL_WINDOWS)
+    lo, hi = window_range(G, world, rank)
+    B = hi - lo
     obs = N * args.emb
     sd = make_state_dict(obs, L, args.hidden, seed=0)
     model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, MODEL_CFG), dev)
@@ -297,13 +412,13 @@ def main():
     std = np.full(N, 0.015, np.float32)
     mean_d = torch.tensor(mean, device=dev)
     std_d = torch.tensor(std, device=dev)
-    torch.manual_seed(1000 + rank)
-    x, wp = make_inputs(B, N, obs, seed=rank, device=dev)
+    x, wp = window_inputs(lo, hi, N, obs, seed=0, device=dev)
     cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, allow_short=False)
 
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
-    def step(e=None):
+    def step(k):
+        e = ev[k] if k is not None else None
         if e is not None:
             e[0].record()
         y = model.rollout(x, mean_d, std_d, H, N)
@@ -313,27 +428,10 @@ def main():
         if e is not None:
             e[2].record()
         if world > 1:
-            gather_rows(W0, world * B, world, rank, dst=0)
+            gather_rows(W0, G, world, rank, dst=0)    # the one RCCL collective
         return y, W0, st, val, its
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        y, W0, st, val, its = step(ev[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, (y, W0, st, val, its) = timed_loop(step, args.steps, args.warmup, world, dev)
 
     roll_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     solve_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -341,48 +439,50 @@ def main():
     n_opt = int((st_np <= 1).sum())
 
     if rank == 0:
-        value = world * B * args.steps / elapsed
-        # algorithmic bytes of one solve launch: read yhat f32 [B,H,N] + w_prev f64 [B,N];
-        # write W0 f64 [B,N] + status i32 + value f64 (+ iters i32) per window
+        value = G * args.steps / elapsed
+        # roofline of the dominant kernel (the solve), SURVEY §8(d): ALGORITHMIC HBM bytes of one
+        # launch — read yhat f32 [B,H,N] + w_prev f64 [B,N]; write W0 f64 [B,N] + status i32 +
+        # value f64 + iters i32 per window — over its HIP-event launch time, against 8 TB/s.
+        # traffic: PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/, scaled to B).
         solve_bytes = B * (4 * H * N + 8 * N + 8 * N + 4 + 8 + 4)
         achieved = solve_bytes / (solve_ms * 1e-3)
-        # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scaled
-        # to this launch's windows) and the executed f64 VALU rate of the solve against its peak:
-        # the solver is bound by f64 latency / VALU, not by HBM
-        traffic, f64_rate = None, None
-        if os.path.exists(PMC_JSON) and (N, H) == (100, 10):
-            pmc = json.load(open(PMC_JSON))
-            traffic = (pmc["fetch_bytes_per_window"] + pmc["write_bytes_per_window"]) * B
-            if "f64_flops_per_window" in pmc:
-                f64_rate = pmc["f64_flops_per_window"] * B / (solve_ms * 1e-3)
-        hbm = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-               "frac": achieved / HBM_PEAK, "traffic": traffic,
-               "algorithmic_bytes_per_window": solve_bytes // B}
-        # The solve kernel is bound by f64 arithmetic issue / latency, not by HBM (it reads each
-        # input once): its roofline is the f64 peak (78.6 TFLOP/s, the same for the
-        # f64 MFMA and the f64 VALU on MI355X), against the executed f64 FLOPs of the launch (PMC
-        # per-window count x windows / HIP-event launch time). The HBM figure stays beside it.
-        if f64_rate is not None:
-            roof = {"bound": "mfma", "achieved": f64_rate / 1e12, "peak": F64_VALU_PEAK / 1e12,
-                    "unit": "TFLOP/s", "frac": f64_rate / F64_VALU_PEAK, "traffic": traffic,
-                    "dtype": "f64", "kernel": "kmpc_solve (ipm_kernel<10,128,true,7,104,true>)", "launch_ms": solve_ms,
-                    "flops": "executed f64 FLOPs per window from PMC (profiles/r02_solve_pmc.json), "
-                             "pipe: f64 VALU (no f64 MFMA use; same 78.6 TFLOP/s peak)"}
-        else:
-            roof = dict(hbm, kernel="kmpc_solve", launch_ms=solve_ms)
+        pmc = json.load(open(PMC_JSON)) if os.path.exists(PMC_JSON) and (N, H) == (100, 10) else None
+        traffic = (pmc["fetch_bytes_per_window"] + pmc["write_bytes_per_window"]) * B if pmc else None
+        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": "kmpc_solve (ipm_kernel, register IPM)",
+                "launch_ms": solve_ms, "algorithmic_bytes_per_window": solve_bytes // B,
+                "windows_per_launch": B}
+        # what actually bounds the solve: f64 issue / latency. Executed f64 FLOPs per window from the
+        # PMC passes (64 lanes x (ADD + MUL + TRANS + 2 FMA) per wave-instruction), scaled by the
+        # active-lane fraction N / blockDim (an upper bound on useful work: wave 0's serial Schur
+        # phases idle more lanes), against the f64 FMA peak measured on this part (profiles/).
+        util = None
+        if pmc and "f64_flops_per_window" in pmc:
+            lanes = pmc.get("active_lane_fraction", N / (64 * -(-N // 64)))
+            useful = pmc["f64_flops_per_window"] * lanes * B / (solve_ms * 1e-3)
+            peak = pmc.get("f64_peak_flops", F64_VALU_PEAK)
+            util = {"pipe": "f64 VALU", "executed_f64_flops_per_window": pmc["f64_flops_per_window"],
+                    "active_lane_fraction": lanes, "achieved": useful / 1e12, "peak": peak / 1e12,
+                    "unit": "TFLOP/s", "frac": useful / peak, "peak_source": pmc.get("f64_peak_source", "spec"),
+                    "counts_from": os.path.relpath(PMC_JSON, ROOT)}
         roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
                                 + H * (L * L + L * N))
+        c4 = world > 1
         line = {
             "metric": METRIC, "value": value, "unit": "windows/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32 rollout / f64 solve",
+            "higher_is_better": True, "scaling": "strong" if c4 else "weak", "vs_baseline": None,
+            "dtype": "f32 rollout / f64 solve",
             "data": "synthetic (seeded N(0,1) standardized embeddings, Dirichlet w_prev, random-init finance_sparse weights)",
-            "config": {"workload": f"C3: {B} windows/GPU, {N} assets, latent {L}, H={H}, obs {obs}, "
-                                   f"GenericKM enc [{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
-                       "windows_per_gpu": B, "global_windows_per_step": world * B,
-                       "parallelism": f"windows sharded over {world} GPU(s), RCCL gather of W0"},
+            "config": {"workload": (f"C4 (BASELINE configs[3]): {G} windows/step over {world} GPUs" if c4 else
+                                    f"C3 (BASELINE configs[2]): {G} windows/GPU") +
+                                   f", {N} assets, latent {L}, H={H}, obs {obs}, GenericKM enc "
+                                   f"[{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
+                       "windows_per_gpu": B, "global_windows_per_step": G,
+                       "parallelism": (f"windows sharded over {world} GPUs (contiguous blocks of one global "
+                                       f"stream), RCCL gather of W0 to rank 0" if c4 else "1 GPU, no collective")},
             "roofline": roof,
-            "hbm_roofline": hbm,
+            "compute_utilization": util,
             # SURVEY.md §8(d)'s whole-path bound: compulsory bytes per window = obs (f32 N d) +
             # w_prev + w0 (f32 as there), weights amortized: windows/s x bytes / 8 TB/s
             "path_hbm_roofline": {"bound": "hbm", "bytes_per_window": 4 * obs + 8 * N,
@@ -402,7 +502,8 @@ def main():
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base
             line["cpu_baseline_serial"] = cpu_baseline_serial(sd, mean, std, x, wp, H, N, cfg,
-                                                              min(5.0, args.cpu_seconds / 4))
+                                                              min(8.0, args.cpu_seconds / 2))
+            line["cpu_baseline_c1"] = cpu_baseline_c1()
             line["cpu_parity"] = parity
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -54,7 +54,8 @@ extern "C" {
  *   maximize_W  sum_t log(R_t . w_t) - c * sum_t ||w_t - w_{t-1}||_1        (mpc.py:66-103)
  *   s.t.        1^T w_t = 1;  w_t >= 0 unless allow_short;                  (mpc.py:83-86)
  *               ||w_t - w_{t-1}||_1 <= tau  if tau > 0, w_{-1} = w_prev     (mpc.py:94-100)
- *   with R_t = exp(yhat_t) (mpc.py:55), W in [H, N].
+ *   with R_t = np.exp(yhat_t) (mpc.py:55) evaluated in float32 exactly as numpy does it
+ *   (kmpc_gross_returns below) and then used in float64, as cvxpy receives it; W in [H, N].
  * Inputs:  yhat [B, H, N] float32 (predicted log-returns, the reference passes float32 here,
  *          backtest.py:121), w_prev [B, N] float64 (current_weights).
  * Outputs: w_out [B, N] (W[0], what rebalance() applies, backtest.py:131) or [B, H, N] when
@@ -63,12 +64,20 @@ extern "C" {
  *          closed-form presolve: cost_coeff = 0, max_turnover <= 0, no shorting, where the
  *          program separates into H simplex problems with a vertex optimum).
  * Failure fallback (mpc.py:113-115) is applied in-kernel: w_out = tile(w_prev), obj = NaN.
- * Workspace: kmpc_workspace_bytes(NULL, desc) bytes (0 for windows of N <= 256 assets and
- *          H <= 10 periods, solved in registers; otherwise the large-window kernel keeps each
- *          window's interior-point state there, ~ (22 H + 128) (64 ceil(N / 64)) doubles per
- *          window for min(B, 768) windows in flight when N <= 256, min(B, 512) otherwise).
+ *          Non-finite yhat / w_prev, or an R that overflows float32 (yhat >= 88.72), give
+ *          solver_error and the fallback.
+ * Errors:  cost_coeff < 0 -> KMPC_ERR_INVALID: the reference program is then not convex
+ *          and cvxpy raises (DCPError) instead of returning a status.
+ * Workspace: always size it with kmpc_workspace_bytes(NULL, desc). It is 0 for windows of
+ *          N <= 256 assets and H <= 10 periods (solved in registers); otherwise the large-window
+ *          kernel keeps each window's interior-point state there: (22 HM + 128) (64 ceil(N / 64))
+ *          doubles per window slot, HM = 10 for H <= 10 and 21 past it (the compiled horizon
+ *          bound, not H), for min(B, 768) slots when N <= 256, min(B, 512) otherwise.
  *          Too little -> KMPC_ERR_WORKSPACE.
  */
+#define KMPC_PATH_AUTO     0   /* kernel chosen by shape (and the closed-form presolve)            */
+#define KMPC_PATH_REGISTER 1   /* interior point in the register kernels where the shape fits them */
+#define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */
@@ -81,6 +90,7 @@ typedef struct kmpc_solve_desc {
     int    return_full_W;  /* 0: w_out is [B,N] (W[0]); 1: w_out is [B,H,N]       */
     int    n_refine;       /* max iterative-refinement steps per Newton solve; refinement stops once
                               ||r||_inf <= 1e-7 ||b||_inf (<0 -> none, 0 -> default 3)             */
+    int    path;           /* KMPC_PATH_* (0 = by shape). Per call: no process-wide switches      */
 } kmpc_solve_desc;
 
 int kmpc_solve(const kmpc_solve_desc* desc,
@@ -91,6 +101,11 @@ int kmpc_solve(const kmpc_solve_desc* desc,
                double*       obj,      /* [B] */
                int*          iters,    /* [B] or NULL */
                void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- gross returns: R = np.exp(yhat) on float32, bit for bit as numpy 2.x evaluates it on x86-64
+ * (mpc.py:55; the realized returns np.exp(r) - 1 of backtest.py:188 use the same function).
+ * yhat and R are device arrays of n floats. */
+int kmpc_gross_returns(size_t n, const float* yhat, float* R, void* stream);
 
 /* ---- Koopman rollout: replaces backtest.py:99-121 (+ model.py encode/step/decode) ---------- */
 #define KMPC_MODEL_GENERIC 0   /* GenericKM / SparseKM (model.py:701-797)                      */
@@ -149,6 +164,8 @@ typedef struct kmpc_rollout_desc {
     int dtype;                /* KMPC_DTYPE_F32 (0, the reference's arithmetic) or KMPC_DTYPE_BF16 (1:
                                  GEMM operands rounded to bf16 on MFMA, fp32 accumulation and
                                  epilogues; BASELINE configs[4])                                 */
+    int latent_unfused;       /* 0: the H-step loop runs as one fused launch where the model allows
+                                 it; 1: one GEMM launch per step (same arithmetic; A/B and tests)  */
 } kmpc_rollout_desc;
 
 int kmpc_rollout(const kmpc_rollout_desc* desc,

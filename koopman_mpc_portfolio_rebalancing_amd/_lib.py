@@ -33,7 +33,9 @@ KMPC_MV_MAX_H = 16
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
                     "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_standardize", "kmpc_strerror",
                     "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments", "kmpc_solve_mv_ws",
-                    "kmpc_mv_workspace_bytes")
+                    "kmpc_mv_workspace_bytes", "kmpc_gross_returns")
+
+PATH_AUTO, PATH_REGISTER, PATH_LARGE = 0, 1, 2   # kmpc_solve_desc.path
 
 
 class KmpcError(RuntimeError):
@@ -44,7 +46,8 @@ class SolveDesc(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_int),
                 ("cost_coeff", ctypes.c_double), ("max_turnover", ctypes.c_double),
                 ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
-                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int), ("n_refine", ctypes.c_int)]
+                ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int), ("n_refine", ctypes.c_int),
+                ("path", ctypes.c_int)]
 
 
 class MvDesc(ctypes.Structure):
@@ -67,7 +70,7 @@ class RolloutDesc(ctypes.Structure):
                 ("encoder", Mlp), ("lista_S", ctypes.c_void_p), ("lista_loops", ctypes.c_int),
                 ("lista_thresh", ctypes.c_float), ("kmat", ctypes.c_void_p), ("decoder", Mlp),
                 ("mean", ctypes.c_void_p), ("std", ctypes.c_void_p), ("obs_ld", ctypes.c_int),
-                ("dtype", ctypes.c_int)]
+                ("dtype", ctypes.c_int), ("latent_unfused", ctypes.c_int)]
 
 
 class BacktestDesc(ctypes.Structure):
@@ -112,6 +115,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_rolling_moments.restype = ctypes.c_int
     L.kmpc_workspace_bytes.argtypes = [ctypes.POINTER(RolloutDesc), ctypes.POINTER(SolveDesc)]
     L.kmpc_workspace_bytes.restype = ctypes.c_size_t
+    L.kmpc_gross_returns.argtypes = [sz, vp, vp, vp]
+    L.kmpc_gross_returns.restype = ctypes.c_int
     L.kmpc_strerror.argtypes = [ctypes.c_int]
     L.kmpc_strerror.restype = ctypes.c_char_p
     L.kmpc_version.argtypes = []

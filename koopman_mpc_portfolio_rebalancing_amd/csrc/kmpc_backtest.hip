@@ -4,7 +4,7 @@
 // One step of run_backtest per path (backtest.py:173-217), after the window solve produced the
 // target weights:
 //   turnover = |target - w|_1;  cost = c * turnover * value;  value -= cost;  w = target
-//   r = exp(y_{t+1}) - 1  (float32, as numpy computes it on the reference's float32 returns)
+//   r = np.exp(y_{t+1}) - 1  (float32: numpy's float32 exp, np_expf, then a float32 subtraction)
 //   port = w . r;  value *= 1 + port;  w = w * (1 + r) / guard(1 + port)   (|.| < 1e-8 -> 1e-8)
 // and the row (value, return, turnover, cost) of the history. The metrics kernel then reduces each
 // path's history exactly as calculate_metrics (population std Sharpe, drawdown on cumprod(1+r),
@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include "kmpc_internal.h"
+#include "kmpc_npexp.h"
 
 namespace kmpc {
 
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(BT_THREADS) bt_step_kernel(StepArgs a) {
         const float* y = a.realized + (size_t)p * a.N;
         double pv = 0.0;
         for (int i = threadIdx.x; i < a.N; i += blockDim.x) {
-            const float r = expf(y[i]) - 1.0f;
+            const float r = np_expf(y[i]) - 1.0f;
             pv += tg[i] * (double)r;
         }
         port = block_sum_bt(pv, red);
@@ -68,7 +69,7 @@ __global__ void __launch_bounds__(BT_THREADS) bt_step_kernel(StepArgs a) {
         double denom = 1.0 + port;
         if (fabs(denom) < 1e-8) denom = 1e-8;
         for (int i = threadIdx.x; i < a.N; i += blockDim.x) {
-            const float g = 1.0f + (expf(y[i]) - 1.0f);
+            const float g = 1.0f + (np_expf(y[i]) - 1.0f);
             w[i] = tg[i] * (double)g / denom;
         }
     } else {
@@ -114,7 +115,19 @@ __global__ void bt_metrics_kernel(int P, int S, const double* hist, double* m) {
     o[4] = h[(S - 1) * 4 + 0] / h[0] - 1.0;
 }
 
+__global__ void gross_returns_kernel(size_t n, const float* __restrict__ y, float* __restrict__ R) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        R[i] = np_expf(y[i]);
+}
+
 }  // namespace
+
+int gross_returns_launch(size_t n, const float* yhat, float* R, hipStream_t stream) {
+    const size_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(gross_returns_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, stream,
+                       n, yhat, R);
+    return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
 
 int backtest_step_launch(const kmpc_backtest_desc* d, int step, const double* target,
                          const float* realized_next, double* weights, double* value, double* hist,

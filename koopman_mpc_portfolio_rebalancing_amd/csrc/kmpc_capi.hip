@@ -14,6 +14,9 @@ int check_solve(const kmpc_solve_desc* d) {
     if (d->B < 0 || d->N < 1 || d->H < 1) return KMPC_ERR_INVALID;
     if (d->N > KMPC_MAX_N || d->H > KMPC_MAX_H) return KMPC_ERR_UNSUPPORTED;
     if (d->H > 21) return KMPC_ERR_UNSUPPORTED;   // Schur system (3H) must fit one wavefront
+    // c < 0 makes -c ||dw||_1 concave in the maximization: not DCP, cvxpy raises (mpc.py:66-103)
+    if (d->cost_coeff < 0.0) return KMPC_ERR_INVALID;
+    if (d->path < KMPC_PATH_AUTO || d->path > KMPC_PATH_LARGE) return KMPC_ERR_INVALID;
     return KMPC_OK;
 }
 
@@ -93,6 +96,12 @@ int kmpc_window(const kmpc_rollout_desc* rdesc, const kmpc_solve_desc* sdesc, co
     if (sdesc->B == 0) return KMPC_OK;
     return kmpc::solve_launch(sdesc, y, w_prev, w_out, status, obj, iters, (char*)workspace + rbytes + ybytes,
                               ws_bytes - rbytes - ybytes, (hipStream_t)stream);
+}
+
+int kmpc_gross_returns(size_t n, const float* yhat, float* R, void* stream) {
+    if (n == 0) return KMPC_OK;
+    if (!yhat || !R) return KMPC_ERR_INVALID;
+    return kmpc::gross_returns_launch(n, yhat, R, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -13,6 +13,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
                  double* trace = nullptr);
 
 // kmpc_backtest.hip
+int gross_returns_launch(size_t n, const float* yhat, float* R, hipStream_t stream);
 int backtest_step_launch(const kmpc_backtest_desc* d, int step, const double* target,
                          const float* realized_next, double* weights, double* value, double* hist,
                          hipStream_t stream);

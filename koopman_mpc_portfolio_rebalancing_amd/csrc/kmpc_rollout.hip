@@ -422,11 +422,12 @@ __global__ void __launch_bounds__(256) latent_steps_kernel(LatentArgs a) {
     }
 }
 
-// debug switch (tools / tests only): 0 runs the H-step loop as separate GEMM launches
-static int g_fused = 1;
-
+// the fused H-step kernel: fp32, one decoder layer, L % 32 == 0 and <= 512 (2 x 32 rows of z in
+// LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
+// descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
 static bool latent_fusable(const kmpc_rollout_desc* d) {
-    return d->dtype == KMPC_DTYPE_F32 && d->decoder.n_layers == 1 && d->L % 32 == 0 && d->L <= 512 &&
+    return !d->latent_unfused && d->dtype == KMPC_DTYPE_F32 && d->decoder.n_layers == 1 && d->L % 32 == 0 &&
+           d->L <= 512 && ((uintptr_t)d->decoder.weight[0] & 15) == 0 &&
            !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn != KMPC_NORM_ID && d->norm_fn != KMPC_NORM_BALL);
 }
 
@@ -563,7 +564,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
 
     // ---- H x (step_latent, decode[:N], destandardize) ----
-    if (g_fused && latent_fusable(d)) {
+    if (latent_fusable(d)) {
         LatentArgs la;
         la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
         la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
@@ -608,9 +609,3 @@ int standardize_launch(int T, int N, const double* y, const double* mean, const 
 }
 
 }  // namespace kmpc
-
-extern "C" int kmpc_debug_rollout_fused(int on) {
-    const int old = kmpc::g_fused;
-    kmpc::g_fused = on;
-    return old;
-}

@@ -9,22 +9,22 @@
 // one problem per period, max log(R_t . w_t) over the simplex, whose optimum is exact in closed
 // form (simplex_kernel below) — BASELINE configs[1], "no-short simplex projection only".
 #include "kmpc_internal.h"
+#include "kmpc_npexp.h"
 #include "kmpc_solve_args.h"
 
 namespace kmpc {
 
 namespace {
 
-// solver path override (debug entry kmpc_debug_solver_path, tools/ A/B only): 0 = by shape,
-// 1 = register kernels whenever they support the shape, 2 = the large-window kernel
-int g_path = 0;
-
+// per-call solver path (kmpc_solve_desc.path): KMPC_PATH_AUTO by shape, KMPC_PATH_REGISTER =
+// interior point in the register kernels whenever they support the shape (no presolve),
+// KMPC_PATH_LARGE = the large-window kernel
 bool simplex_case(const SolveArgs& a) {
-    return g_path == 0 && !(a.c > 0.0) && !(a.tau > 0.0) && !a.allow_short;
+    return a.path == KMPC_PATH_AUTO && !(a.c > 0.0) && !(a.tau > 0.0) && !a.allow_short;
 }
 
 // c = tau = 0, w >= 0: per period t, log(R_t . w_t) with R = exp(yhat) > 0 is maximized over the
-// simplex exactly on the face of the assets with the largest yhat_t; the returned point is that
+// simplex exactly on the face of the assets with the largest R_t; the returned point is that
 // face's centre (equal weights over exact ties: the analytic centre an interior-point method
 // converges to, and the vertex e_argmax otherwise). problem.value as the IPM kernels report it
 // (mpc.py:103): sum_t log(R_t . w_t) - c sum_t ||w_t - w_{t-1}||_1 (c <= 0 here). One wave per
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a
     double* wout = a.wout + (size_t)b * tw * N;
     int bad = !(isfinite(a.c) && isfinite(a.tau));
     for (int i = lane; i < N; i += 64) bad |= !isfinite(wp[i]);
-    for (int k = lane; k < H * N; k += 64) bad |= !isfinite(y[k]);
+    for (int k = lane; k < H * N; k += 64) bad |= !isfinite(np_expf(y[k]));
     if (wsumi(bad)) {
         for (int k = lane; k < tw * N; k += 64) wout[k] = wp[k % N];   // mpc.py:113-115
         if (lane == 0) {
@@ -63,28 +63,31 @@ __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a
         }
         return;
     }
+    // the face is that of the largest float32 R = np.exp(yhat) (mpc.py:55): distinct yhat can
+    // round to the same R, and the program the reference solves only sees R
     double f = 0.0;
-    float pym = 0.0f;
+    float prm = 0.0f;
     double pw = 0.0;   // the previous period's face weight
     for (int t = 0; t < H; ++t) {
         const float* yt = y + (size_t)t * N;
-        float ym = -INFINITY;
-        for (int i = lane; i < N; i += 64) ym = fmaxf(ym, yt[i]);
-        ym = wmaxf(ym);
+        float rm = 0.0f;
+        for (int i = lane; i < N; i += 64) rm = fmaxf(rm, np_expf(yt[i]));
+        rm = wmaxf(rm);
         int cnt = 0;
-        for (int i = lane; i < N; i += 64) cnt += yt[i] == ym;
+        for (int i = lane; i < N; i += 64) cnt += np_expf(yt[i]) == rm;
         cnt = wsumi(cnt);
         const double w = 1.0 / cnt;
         double rw = 0.0, l1 = 0.0;
         for (int i = lane; i < N; i += 64) {
-            const double wi = yt[i] == ym ? w : 0.0;
-            rw += (1.0 + expm1((double)yt[i])) * wi;
-            const double wprev = t == 0 ? wp[i] : (y[(size_t)(t - 1) * N + i] == pym ? pw : 0.0);
+            const float ri = np_expf(yt[i]);
+            const double wi = ri == rm ? w : 0.0;
+            rw += (double)ri * wi;
+            const double wprev = t == 0 ? wp[i] : (np_expf(y[(size_t)(t - 1) * N + i]) == prm ? pw : 0.0);
             l1 += fabs(wi - wprev);
             if (t < tw) wout[(size_t)t * N + i] = wi;
         }
         f += log(wsum(rw)) - a.c * wsum(l1);
-        pym = ym;
+        prm = rm;
         pw = w;
     }
     if (lane == 0) {
@@ -104,6 +107,7 @@ SolveArgs make_args(const kmpc_solve_desc* d) {
     a.tol = d->tol > 0.0 ? d->tol : 1e-9;
     a.return_full = d->return_full_W;
     a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 3);
+    a.path = d->path;
     return a;
 }
 
@@ -111,8 +115,8 @@ bool use_big(const SolveArgs& a) {
 #ifdef KMPC_DEV_ONLY_H10
     return false;
 #else
-    if (g_path == 1) return false;
-    if (g_path == 2) return true;
+    if (a.path == KMPC_PATH_REGISTER) return false;
+    if (a.path == KMPC_PATH_LARGE) return true;
     // measured on MI355X (tools/path_ab.py): the register kernels win up to 256 assets at
     // H <= 10 (N = 192: 76k vs 41k windows/s); the large-window kernel wins past 10 periods at any
     // N (N = 100, H = 20: 36k vs 24k) and past 256 assets (N = 500, H = 10: 23k vs 13k)
@@ -166,9 +170,3 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
 }
 
 }  // namespace kmpc
-
-extern "C" int kmpc_debug_solver_path(int path) {
-    const int old = kmpc::g_path;
-    kmpc::g_path = path;
-    return old;
-}

@@ -8,6 +8,7 @@ struct SolveArgs {
     int B, N, H;
     double c, tau;
     int allow_short, max_iter, return_full, n_refine;
+    int path;        // kmpc_solve_desc.path (KMPC_PATH_*)
     double tol;
     const float* yhat;
     const double* wp;

@@ -1017,14 +1017,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         const int tw = a.return_full ? H : 1;
         W.wpi = W.act ? wp[i] : 0.0;
 
-        // ---- inputs: m = expm1(yhat) (slab), objective scale, finiteness ----
+        // ---- inputs: m = R - 1, R = np.exp(yhat) in float32 (mpc.py:55; slab), objective scale,
+        //      finiteness (non-finite yhat or overflowing R -> solver_error) ----
         double mx = 0.0, nf = 0.0;
         if (W.act) {
             if (!isfinite(W.wpi)) nf = 1.0;
             for (int t = 0; t < H; ++t) {
-                const double y = (double)yh[t * N + i];
-                if (!isfinite(y)) nf = 1.0;
-                const double m = expm1(y);
+                const double m = np_expm1_d(yh[t * N + i]);
+                if (!isfinite(m)) nf = 1.0;
                 W.at(A_M, t) = m;
                 mx = fmax(mx, fabs(m));
             }

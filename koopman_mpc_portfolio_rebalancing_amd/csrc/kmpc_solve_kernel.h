@@ -33,6 +33,7 @@
 #include <utility>
 
 #include "kmpc_internal.h"
+#include "kmpc_npexp.h"
 #include "kmpc_solve_args.h"
 
 namespace kmpc {
@@ -1331,7 +1332,7 @@ __device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM>& R, 
         rw[t] = l1n[t] = 0.0;
         if (T.act && t < H) {
             if (t < tw) wout[t * N + T.i] = T.w[t];
-            rw[t] = (1.0 + T.m[t]) * T.w[t];   // exp(yhat) = 1 + expm1(yhat)
+            rw[t] = (1.0 + T.m[t]) * T.w[t];   // R = 1 + m exactly
             l1n[t] = fabs(T.w[t] - T.wprev(t));
         }
     }
@@ -1365,16 +1366,16 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
     const float* yh = args.yhat + (size_t)b * H * N;
     T.wpi = T.act ? wp[T.i] : 0.0;
 
-    // ---- inputs: m = expm1(yhat), objective scale, finiteness ----
+    // ---- inputs: m = R - 1 with R = np.exp(yhat) in float32 (mpc.py:55), objective scale,
+    //      finiteness (a non-finite yhat or an overflowing R -> solver_error) ----
     double mx = 0.0;
     bool finite = true;
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         T.m[t] = 0.0;
         if (T.act && t < H) {
-            const double y = (double)yh[t * N + T.i];
-            finite = finite && isfinite(y);
-            T.m[t] = expm1(y);
+            T.m[t] = np_expm1_d(yh[t * N + T.i]);
+            finite = finite && isfinite(T.m[t]);
             mx = fmax(mx, fabs(T.m[t]));
         }
     }

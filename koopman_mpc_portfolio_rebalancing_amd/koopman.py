@@ -110,9 +110,12 @@ class KoopmanModelSpec:
 class DeviceKoopman:
     """A KoopmanModelSpec resident on one device, evaluated through kmpc_rollout / kmpc_window."""
 
-    def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None, dtype: str = "fp32"):
+    def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None, dtype: str = "fp32",
+                 fuse_latent: bool = True):
         """dtype: 'fp32' (the reference's arithmetic, default) or 'bf16' (GEMM operands rounded to
-        bf16 on the bf16 MFMA, fp32 accumulation — BASELINE configs[4])."""
+        bf16 on the bf16 MFMA, fp32 accumulation — BASELINE configs[4]). fuse_latent=False runs the
+        H-step loop as one GEMM launch per step (kmpc_rollout_desc.latent_unfused; A/B and tests)."""
+        self.fuse_latent = bool(fuse_latent)
         if dtype not in _lib.DTYPE:
             raise ValueError(f"dtype must be one of {sorted(_lib.DTYPE)}")
         self.dtype = dtype
@@ -134,7 +137,6 @@ class DeviceKoopman:
         self.S = up(spec.lista_S)
         if len(self.enc) > _lib.KMPC_MAX_LAYERS or len(self.dec) > _lib.KMPC_MAX_LAYERS:
             raise _lib.KmpcError("too many layers for kmpc_mlp")
-        self._ws = {}   # workspace per HIP stream (kmpc.h: calls are stream-ordered)
 
     @property
     def latent(self) -> int:
@@ -166,6 +168,7 @@ class DeviceKoopman:
         d.encoder = self._mlp(enc if enc is not None else self.enc, s.enc_act, s.enc_last_relu)
         d.obs_ld = int(obs_ld)
         d.dtype = _lib.DTYPE[self.dtype]
+        d.latent_unfused = int(not self.fuse_latent)
         d.lista_S = self.S.data_ptr() if self.S is not None else None
         d.lista_loops = int(s.lista_loops)
         d.lista_thresh = float(s.lista_thresh)
@@ -176,15 +179,9 @@ class DeviceKoopman:
         return d
 
     def _workspace(self, nbytes: int) -> torch.Tensor:
-        """Scratch for one call, private to the caller's current stream: calls issued on
-        different streams never share (and overwrite) a workspace. torch's caching allocator
-        keeps each buffer alive for its stream."""
-        key = _lib.stream_handle(self.device) or 0
-        ws = self._ws.get(key)
-        if ws is None or ws.numel() < nbytes:
-            ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
-            self._ws[key] = ws
-        return ws
+        """Scratch for one call from torch's caching allocator on the current stream (reused in
+        stream order once dropped; nothing is held between calls)."""
+        return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
 
     def _check_obs(self, x: torch.Tensor) -> None:
         if x.dim() != 2 or x.shape[1] != self.obs_size:

@@ -34,6 +34,7 @@ class MPCConfig:
     max_iter: int = 80
     tol: float = 1e-9
     n_refine: int = 0  # 0 -> kernel default
+    solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM
 
 
 def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:
@@ -46,30 +47,18 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     d.tol = float(getattr(config, "tol", 1e-9))
     d.return_full_W = int(bool(full))
     d.n_refine = int(getattr(config, "n_refine", 0))
+    d.path = int(getattr(config, "solver_path", 0))
+    if d.cost_coeff < 0:
+        # -c ||dw||_1 with c < 0 is not concave: the reference's cvxpy problem fails DCP and raises
+        raise ValueError(f"cost_coeff must be >= 0 (got {config.cost_coeff}): the problem is not convex")
     return d
 
 
-_WS = {}   # solve workspaces per (device, HIP stream): calls on different streams never share one
-
-
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    """A device buffer of at least nbytes, cached per (device, current HIP stream)."""
-    key = (device.index, _lib.stream_handle(device) or 0)
-    ws = _WS.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        _WS[key] = ws
-    return ws
-
-
-def _solve_workspace(d: _lib.SolveDesc, device: torch.device) -> Tuple[int, int]:
-    """(pointer, bytes) of a workspace large enough for the solve described by d (the large-window
-    kernel keeps each window's interior-point state there; the register kernels need none)."""
-    nbytes = int(_lib.load().kmpc_workspace_bytes(None, ctypes.byref(d)))
-    if nbytes == 0:
-        return 0, 0
-    ws = _workspace(device, nbytes)
-    return ws.data_ptr(), ws.numel()
+    """A device buffer of at least nbytes for one call, from torch's caching allocator on the
+    current stream: the block returns to the pool when the caller drops it and is handed out again
+    only in stream order, so concurrent streams never share scratch and nothing is held between calls."""
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
 def solve_mpc_log_utility_batched(
@@ -110,10 +99,11 @@ def solve_mpc_log_utility_batched(
     d = _solve_desc(B, N, H, config, return_full)
     L = _lib.load()
     with torch.cuda.device(y.device):
-        ws, nws = _solve_workspace(d, y.device)
+        nws = int(L.kmpc_workspace_bytes(None, ctypes.byref(d)))
+        ws = _workspace(y.device, nws) if nws else None
         rc = L.kmpc_solve(ctypes.byref(d), y.data_ptr(), wp.data_ptr(), W.data_ptr(),
-                          status.data_ptr(), value.data_ptr(), iters.data_ptr(), ws or None, nws,
-                          _lib.stream_handle(y.device))
+                          status.data_ptr(), value.data_ptr(), iters.data_ptr(),
+                          ws.data_ptr() if ws is not None else None, nws, _lib.stream_handle(y.device))
     _lib.check(rc)
     if with_iters:
         return W, status, value, iters

@@ -8,8 +8,9 @@ Two deliberately simple float64 solvers of the program in ``mpc.py:49-117`` of t
 * :func:`slsqp`      — scipy SLSQP on the lifted L1 form ``w_t - w_{t-1} = u_t - v_t``, u, v >= 0,
   i.e. an algorithm unrelated to interior points.
 
-Both use the reference's objective verbatim: ``sum_t log(w_t . exp(y_t)) - c sum_t ||w_t - w_{t-1}||_1``
-(mpc.py:55, 66-103), constraints ``sum w_t = 1`` (mpc.py:83), ``w >= 0`` unless allow_short
+Both use the reference's objective verbatim: ``sum_t log(w_t . R_t) - c sum_t ||w_t - w_{t-1}||_1``
+with ``R = np.exp(yhat)`` evaluated on the float32 yhat exactly as the reference does (mpc.py:55;
+cvxpy then works with R in float64) (mpc.py:66-103), constraints ``sum w_t = 1`` (mpc.py:83), ``w >= 0`` unless allow_short
 (mpc.py:85-86) and ``||w_t - w_{t-1}||_1 <= tau`` when tau > 0 (mpc.py:94-100).
 """
 from __future__ import annotations
@@ -17,10 +18,15 @@ from __future__ import annotations
 import numpy as np
 
 
+def gross_returns(y):
+    """R = np.exp(yhat) on the float32 yhat (mpc.py:55), promoted to float64 as cvxpy sees it."""
+    return np.exp(np.asarray(y, np.float32)).astype(np.float64)
+
+
 def reference_objective(W, w_prev, y, cost):
     """problem.value of mpc.py:103 evaluated at W (float64)."""
     W = np.asarray(W, np.float64)
-    R = np.exp(np.asarray(y, np.float64))
+    R = gross_returns(y)
     f = float(np.sum(np.log(np.einsum("hn,hn->h", R, W))))
     prev = np.asarray(w_prev, np.float64)
     for t in range(W.shape[0]):
@@ -74,9 +80,9 @@ def _build(wp, y, c, tau, allow_short):
 def dense_ipm(w_prev, y, cost, tau, allow_short=False, iters=100, tol=1e-12):
     """Dense-KKT Mehrotra IPM. Returns (W [H,N], converged: bool)."""
     wp = np.asarray(w_prev, np.float64)
+    m = gross_returns(y) - 1.0  # log(R.w) == log(1 + m.w) on sum(w) = 1
     y = np.asarray(y, np.float64)
     H, N = y.shape
-    m = np.expm1(y)  # log(R.w) == log(1 + m.w) on sum(w) = 1
     G, h, A, b, cvec, nw = _build(wp, y, cost, tau, allow_short)
     nx = G.shape[1]
     mi = G.shape[0]
@@ -140,9 +146,9 @@ def slsqp(w_prev, y, cost, tau, allow_short=False):
     from scipy.optimize import minimize
 
     wp = np.asarray(w_prev, np.float64)
+    R = gross_returns(y)
     y = np.asarray(y, np.float64)
     H, N = y.shape
-    R = np.exp(y)
     n = H * N
 
     def unpack(v):

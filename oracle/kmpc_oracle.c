@@ -7,7 +7,8 @@
  * CPU restatement of the reference's per-window MPC solve:
  *
  *   solve_mpc_log_utility(current_weights, predicted_log_returns, config)   mpc.py:27-117
- *     R = exp(yhat)                                                          mpc.py:55
+ *     R = np.exp(yhat)  on the float32 yhat (backtest.py:121), numpy's float32 exp,   mpc.py:55
+ *                       promoted to float64 by cvxpy (np_expf below)
  *     maximize  sum_t log(w_t . R_t) - c * sum_t ||w_t - w_{t-1}||_1         mpc.py:66-103
  *     s.t.      sum(w_t) == 1                                                mpc.py:83
  *               w_t >= 0                     if not allow_short              mpc.py:85-86
@@ -19,7 +20,7 @@
  * here, so the oracle restates the PROGRAM (its optimum), not SCS's iteration: a Mehrotra
  * predictor-corrector primal-dual interior-point method on the epigraph form
  *
- *   min  -(1/sig) sum_t log(1 + m_t.w_t) + (c/sig) sum_t 1's_t      m = expm1(yhat)
+ *   min  -(1/sig) sum_t log(1 + m_t.w_t) + (c/sig) sum_t 1's_t      m = (double)R - 1 (exact)
  *   s.t. w >= 0,  s_t - d_t >= 0,  s_t + d_t >= 0,  tau - 1's_t >= 0,  1'w_t = 1,
  *        d_t = w_t - w_{t-1},  w_{-1} = w_prev,
  *
@@ -62,6 +63,43 @@ typedef double real;
 #define API(name) name
 #endif
 #define RISFIN(x) isfinite(x)
+
+/*
+ * numpy's float32 exp (numpy 2.x, x86-64 AVX2 / AVX512F: simd_exp_f32 in
+ * numpy/_core/src/umath/loops_exponent_log.dispatch.c.src) — the function that produces the
+ * reference's R at mpc.py:55 and its realized returns np.exp(r) - 1 at backtest.py:188. Restated
+ * from its published algorithm: saturation at x >= 88.7228 (+inf) and x <= -103.972 (0);
+ * k = rint(x log2 e) by the 1.5*2^23 magic round in float32; Cody-Waite reduction
+ * r = x - k ln2 (ln2 split high/low) in float32 FMAs; exp(r) ~ P5(r)/Q2(r) (Remez), Horner in
+ * float32 FMAs and one correctly rounded float32 division; scaling by 2^k. Bit-identical to np.exp
+ * on every finite float32 with |x| < 100 (checked exhaustively in the build container;
+ * tests/test_oracle.py::test_np_expf_restatement_is_bit_exact re-checks 2^24 of them). The
+ * volatile temporaries keep the compiler from contracting x*log2e + magic into an FMA.
+ */
+static float np_expf(float x) {
+    if (x != x) return x;
+    if (x >= 88.72283935546875f) return INFINITY;
+    if (x <= -103.97208404541015625f) return 0.0f;
+    volatile float q0 = x * 1.442695040888963407359924681001892137f;
+    volatile float q1 = q0 + 0x1.8p+23f;
+    const float q = q1 - 0x1.8p+23f;
+    float r = fmaf(q, -6.93145752e-1f, x);
+    r = fmaf(q, -1.42860677e-6f, r);
+    r = fmaf(q, 0.0f, r);
+    float p = fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+    p = fmaf(p, r, 5.114512081637298353406e-02f);
+    p = fmaf(p, r, 2.473615434895520810817e-01f);
+    p = fmaf(p, r, 7.257664613233124478488e-01f);
+    p = fmaf(p, r, 9.999999999980870924916e-01f);
+    float d = fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+    d = fmaf(d, r, 1.0f);
+    volatile float e = p / d;
+    return ldexpf(e, (int)q);
+}
+
+void kmpc_oracle_gross_returns(long n, const float* y, float* R) {
+    for (long k = 0; k < n; ++k) R[k] = np_expf(y[k]);
+}
 
 #define ST_OPTIMAL 0
 #define ST_INACCURATE 1
@@ -458,7 +496,7 @@ double API(kmpc_oracle_objective)(int N, int H, const double* wp, const float* y
     for (int t = 0; t < H; ++t) {
         double rw = 0, l1 = 0;
         for (int i = 0; i < N; ++i) {
-            rw += exp((double)yhat[t * N + i]) * Wm[t * N + i];
+            rw += (double)np_expf(yhat[t * N + i]) * Wm[t * N + i];
             l1 += fabs(Wm[t * N + i] - (t ? Wm[(t - 1) * N + i] : wp[i]));
         }
         f += log(rw) - c * l1;
@@ -476,7 +514,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
     if (max_iter <= 0) max_iter = 80;
     if (tol <= 0) tol = 1e-11;
     int finite = isfinite(c) && isfinite(tau);
-    for (size_t k = 0; k < HN; ++k) finite &= isfinite(yhat[k]) != 0;
+    for (size_t k = 0; k < HN; ++k) finite &= isfinite(np_expf(yhat[k])) != 0;   /* R finite */
     for (int i = 0; i < N; ++i) finite &= isfinite(wp[i]) != 0;
 
     ws_t W;
@@ -488,7 +526,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
         real sig = c;
         for (int i = 0; i < N; ++i) W.wp[i] = wp[i];
         for (size_t k = 0; k < HN; ++k) {
-            W.m[k] = (real)expm1((double)yhat[k]);
+            W.m[k] = (real)((double)np_expf(yhat[k]) - 1.0);   /* exact: R has 24 bits */
             if (RFABS(W.m[k]) > sig) sig = RFABS(W.m[k]);
         }
         if (!(sig > 0)) sig = 1;

@@ -50,7 +50,10 @@ def lib(precision: str = "ld"):
         batch_f.restype = ctypes.c_int
         obj_f.argtypes = [ctypes.c_int, ctypes.c_int, dp, fp, ctypes.c_double, dp]
         obj_f.restype = ctypes.c_double
-        _libs[precision] = (solve_f, batch_f, obj_f)
+        gr_f = L.kmpc_oracle_gross_returns
+        gr_f.argtypes = [ctypes.c_long, fp, fp]
+        gr_f.restype = None
+        _libs[precision] = (solve_f, batch_f, obj_f, gr_f)
     return _libs[precision]
 
 
@@ -99,3 +102,11 @@ def objective(W, w_prev, yhat, cost_coeff):
     H, N = y.shape
     return float(lib()[2](N, H, _p(wp, ctypes.c_double), _p(y, ctypes.c_float),
                                              float(cost_coeff), _p(W, ctypes.c_double)))
+
+
+def gross_returns(yhat):
+    """R = np.exp(yhat) in float32 by the oracle's restatement of numpy's float32 exp."""
+    y = np.ascontiguousarray(yhat, np.float32)
+    R = np.empty_like(y)
+    lib("d")[3](y.size, _p(y, ctypes.c_float), _p(R, ctypes.c_float))
+    return R

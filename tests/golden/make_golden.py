@@ -8,7 +8,8 @@ What it records (all float data, no code):
   rollout_*.npz   reference model.py weights (seeded init), observations, stats, and the yhat the
                   reference KoopmanMPCStrategy.rebalance loop computes (backtest.py:99-121) using the
                   reference's own model / FinanceEnv methods.
-  mpc_*.npz       MPC problems (w_prev, yhat, config) with the long-double oracle optimum
+  mpc_*.npz       MPC problems (w_prev, yhat, numpy's float32 R = np.exp(yhat), config) with the
+                  long-double oracle optimum
                   (oracle/kmpc_oracle.c), plus SLSQP / dense-IPM cross-checks where small enough.
   backtest_*.npz  reference run_backtest + calculate_metrics (backtest.py:133-249) on a synthetic
                   FinanceEnv built with the reference's data_finance functions; the MPC solve inside
@@ -210,8 +211,10 @@ def make_mpc_goldens():
             Wd = np.stack([dense_ipm.dense_ipm(wp[b], y[b], c, tau, short)[0] for b in range(B)])
             Ws = np.stack([dense_ipm.slsqp(wp[b], y[b], c, tau, short)[0] for b in range(B)])
             extra = {"W_dense": Wd, "W_slsqp": Ws}
-        np.savez_compressed(os.path.join(HERE, f"mpc_{name}.npz"), w_prev=wp, yhat=y, W=W, status=st, obj=obj,
-                            iters=it, config=np.array([c, tau, float(short)]), **extra)
+        # R: the gross returns exactly as the reference forms them (np.exp on the float32 yhat,
+        # mpc.py:55) — what cvxpy receives, after promotion to float64
+        np.savez_compressed(os.path.join(HERE, f"mpc_{name}.npz"), w_prev=wp, yhat=y, R=np.exp(y), W=W, status=st,
+                            obj=obj, iters=it, config=np.array([c, tau, float(short)]), **extra)
         print("mpc", name, np.bincount(st, minlength=5), int(it.max()))
 
 

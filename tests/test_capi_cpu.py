@@ -42,6 +42,13 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -2
     d.H, d.B = 5, 0
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == 0
+    d.cost_coeff = -1e-3                   # not convex: cvxpy raises, the boundary rejects it
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d.cost_coeff, d.path = 0.0, 7           # unknown solver path
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d.path = 0
+    assert lib.kmpc_gross_returns(0, None, None, None) == 0
+    assert lib.kmpc_gross_returns(4, None, None, None) == -1
     bt = _lib.BacktestDesc(2, 3, 4, 1e-3)
     assert lib.kmpc_backtest_step(ctypes.byref(bt), 4, None, None, None, None, None, None) == -1   # step >= S
     assert lib.kmpc_backtest_step(ctypes.byref(bt), 0, None, None, None, None, None, None) == -1   # null arrays
@@ -65,13 +72,15 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu\\n", sizeof(kmpc_solve_desc), offsetof(kmpc_solve_desc, tol),
-         offsetof(kmpc_solve_desc, return_full_W), offsetof(kmpc_solve_desc, max_turnover));
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_solve_desc), offsetof(kmpc_solve_desc, tol),
+         offsetof(kmpc_solve_desc, return_full_W), offsetof(kmpc_solve_desc, max_turnover),
+         offsetof(kmpc_solve_desc, path));
   printf("%zu %zu %zu\\n", sizeof(kmpc_mlp), offsetof(kmpc_mlp, weight), offsetof(kmpc_mlp, bias));
   printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
          offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
          offsetof(kmpc_rollout_desc, std));
-  printf("%zu %zu\\n", offsetof(kmpc_rollout_desc, obs_ld), offsetof(kmpc_rollout_desc, dtype));
+  printf("%zu %zu %zu\\n", offsetof(kmpc_rollout_desc, obs_ld), offsetof(kmpc_rollout_desc, dtype),
+         offsetof(kmpc_rollout_desc, latent_unfused));
   printf("%zu %zu\\n", sizeof(kmpc_backtest_desc), offsetof(kmpc_backtest_desc, cost_coeff));
   printf("%zu %zu %zu %zu\\n", sizeof(kmpc_mv_desc), offsetof(kmpc_mv_desc, gamma),
          offsetof(kmpc_mv_desc, tol), offsetof(kmpc_mv_desc, return_full_W));
@@ -82,10 +91,10 @@ int main(void) {{
     subprocess.run(["gcc", str(prog), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     S, M, R, Bt, Mv = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc, _lib.BacktestDesc, _lib.MvDesc
-    expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset,
+    expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset, S.path.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
               ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
-              R.obs_ld.offset, R.dtype.offset,
+              R.obs_ld.offset, R.dtype.offset, R.latent_unfused.offset,
               ctypes.sizeof(Bt), Bt.cost_coeff.offset,
               ctypes.sizeof(Mv), Mv.gamma.offset, Mv.tol.offset, Mv.return_full_W.offset]
     assert [int(x) for x in out] == expect

@@ -100,3 +100,46 @@ def test_status_and_fallback_semantics():
     # shorting allowed, no cost, no cap: log utility unbounded
     W, st, obj, _ = solver.solve([0.5, 0.5], y, 0.0, 0.0, allow_short=True)
     assert solver.STATUS_NAMES[st] == "unbounded" and np.array_equal(W, [[0.5, 0.5]])
+
+
+def test_np_expf_restatement_is_bit_exact():
+    """The oracle's restatement of numpy's float32 exp (R = np.exp(yhat), mpc.py:55) against np.exp
+    itself: 2^24 random float32 bit patterns (every exponent, saturation, NaN/inf) and a dense
+    sweep of log-return-sized inputs. (Exhaustively equal over |x| < 100 when it was written.)"""
+    rng = np.random.default_rng(11)
+    bits = rng.integers(0, 2 ** 32, 1 << 24, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(np.float32)
+    dense = np.linspace(-0.5, 0.5, 1 << 22, dtype=np.float32)
+    for v in (x, dense, np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 88.72283935546875, 88.7228, -103.97208404541015625,
+                                  -103.972, 1e-30, -1e-30], np.float32)):
+        with np.errstate(over="ignore", invalid="ignore"):
+            ref = np.exp(v)
+        got = solver.gross_returns(v)
+        same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+        assert same.all(), v[~same][:8]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mpc_*_*.npz"))))
+def test_golden_gross_returns_are_numpys(path):
+    """Each MPC golden records R = np.exp(yhat) as numpy computed it when the fixture was made; the
+    oracle's R (the one its optimum is computed from) is that array bit for bit."""
+    g = np.load(path)
+    if "R" not in g.files:
+        pytest.skip("known-answer file")
+    assert g["R"].dtype == np.float32
+    assert np.array_equal(solver.gross_returns(g["yhat"]).view(np.uint32), g["R"].view(np.uint32))
+
+
+def test_float32_gross_return_ties_decide_the_optimum():
+    """yhat that differ but round to the same float32 R (mpc.py:55) give the reference a flat
+    objective between those assets: with the turnover cap the optimum set is the whole feasible
+    segment and the interior point returns its centre w_prev, not the vertex a float64 exp(yhat)
+    would favour ([0.6, 0.4] at the cap)."""
+    y = np.array([[0.01, np.nextafter(np.float32(0.01), np.float32(0))]], np.float32)
+    assert y[0, 0] != y[0, 1] and np.exp(y)[0, 0] == np.exp(y)[0, 1]
+    W, st, obj, _ = solver.solve([0.5, 0.5], y, 0.0, 0.2)
+    assert st == 0 and np.abs(W[0] - 0.5).max() < 1e-6
+    assert obj == pytest.approx(float(np.log(np.float64(np.exp(y)[0, 0]))), abs=1e-15)
+    # with float64 exp the larger yhat would win up to the cap
+    Wd, _ = dense_ipm.dense_ipm([0.5, 0.5], y, 0.0, 0.2)
+    assert np.abs(Wd[0] - 0.5).max() < 1e-6

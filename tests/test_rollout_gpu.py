@@ -203,13 +203,12 @@ def test_bf16_lista_rollout_at_config5_shape():
 
 
 @pytest.mark.parametrize("norm,L,N,B,H", [("id", 64, 20, 1000, 4), ("ball", 64, 40, 333, 3),
-                                          ("id", 128, 30, 4096, 5), ("ball", 256, 100, 70, 10)])
+                                          ("id", 128, 30, 4096, 5), ("ball", 256, 100, 70, 10),
+                                          ("id", 512, 50, 300, 6)])   # L = 512: 132 KB of LDS
 def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
     """The one-launch H-step loop (latent_steps_kernel: L % 32 == 0, single-layer decoder) against
     the per-step GEMM launches (debug switch) and the numpy restatement."""
-    import ctypes
     import bench
-    from koopman_mpc_portfolio_rebalancing_amd import _lib
     obs, hidden = N * 4, 64
     sd = bench.make_state_dict(obs, L, hidden, seed=3)
     cfg = {"MODEL": dict(bench.MODEL_CFG["MODEL"], NORM_FN=norm)}
@@ -218,13 +217,8 @@ def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
     mean = np.linspace(-1e-3, 1e-3, N).astype(np.float32)
     std = np.linspace(0.01, 0.02, N).astype(np.float32)
     yf = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
-    lib = _lib.load()
-    lib.kmpc_debug_rollout_fused.argtypes = [ctypes.c_int]
-    old = lib.kmpc_debug_rollout_fused(0)
-    try:
-        yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
-    finally:
-        lib.kmpc_debug_rollout_fused(old)
+    km.fuse_latent = False                     # kmpc_rollout_desc.latent_unfused: per-step launches
+    yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
     sdn = {k: v.numpy() for k, v in sd.items()}
     spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
                "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],

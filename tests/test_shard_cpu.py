@@ -64,3 +64,57 @@ def test_sharded_solve_equals_single_process(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), out, wp, y), nprocs=2, join=True)
     ref = _solve_block(wp, y).numpy()
     assert np.array_equal(np.load(out), ref)
+
+
+def _stub_step_factory(lo, hi, G, world, rank, N, obs):
+    """bench.py's per-rank step with a deterministic CPU stand-in for rollout + solve: inputs from
+    the global stream (bench.window_inputs), per-window 'weights' from (obs, w_prev), then the
+    bench's gather of W0 to rank 0 (shard.gather_rows)."""
+    import bench
+    x, wp = bench.window_inputs(lo, hi, N, obs, seed=0, device=torch.device("cpu"))
+
+    def step(k):
+        s = torch.softmax(x[:, :N].double(), dim=1)
+        W0 = 0.5 * s + 0.5 * wp                      # stays on the simplex, depends on both inputs
+        return gather_rows(W0, G, world, rank, dst=0)
+    return step
+
+
+def _bench_worker(rank, world, port, out_path, G, N, obs):
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = window_range(G, world, rank)
+        step = _stub_step_factory(lo, hi, G, world, rank, N, obs)
+        elapsed, W0 = bench.timed_loop(step, 3, 1, world, torch.device("cpu"))
+        # every rank holds the same max-over-ranks elapsed time
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        ts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(ts, t)
+        assert all(float(v) == elapsed for v in ts) and elapsed > 0
+        if rank == 0:
+            np.save(out_path, W0.numpy())
+        else:
+            assert W0 is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_sharded_path_equals_single_process(tmp_path):
+    """bench.py's distributed branch on gloo, world 2: ragged blocks of one global window stream,
+    the timed loop (barriers, max-over-ranks elapsed) and the W0 gather — the gathered W0 equals
+    the world-1 result bit for bit, and the stream's blocks are the rows of the whole batch."""
+    import bench
+    G, N, obs = 9000, 7, 12                      # ragged: 4500 / 4500 over two ranks, chunk-crossing
+    x_all, wp_all = bench.window_inputs(0, G, N, obs, seed=0, device=torch.device("cpu"))
+    for lo, hi in (window_range(G, 3, 1), (4095, 4097), (0, 1)):
+        xb, wb = bench.window_inputs(lo, hi, N, obs, seed=0, device=torch.device("cpu"))
+        assert torch.equal(xb, x_all[lo:hi]) and torch.equal(wb, wp_all[lo:hi])
+    assert torch.allclose(wp_all.sum(1), torch.ones(G, dtype=torch.float64)) and (wp_all > 0).all()
+    out = str(tmp_path / "w0.npy")
+    mp.spawn(_bench_worker, args=(2, _free_port(), out, G, N, obs), nprocs=2, join=True)
+    step1 = _stub_step_factory(0, G, G, 1, 0, N, obs)
+    _, ref = bench.timed_loop(step1, 1, 0, 1, torch.device("cpu"))
+    assert np.array_equal(np.load(out), ref.numpy())

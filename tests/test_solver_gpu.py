@@ -20,9 +20,9 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _solve(wp, y, c, tau, short=False, full=True):
+def _solve(wp, y, c, tau, short=False, full=True, path=0):
     H = y.shape[1]
-    cfg = MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, allow_short=short)
+    cfg = MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, allow_short=short, solver_path=path)
     W, st, val = solve_mpc_log_utility_batched(torch.tensor(wp, device="cuda"), torch.tensor(y, device="cuda"),
                                                cfg, return_full=full)
     return W.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy()
@@ -122,14 +122,13 @@ def test_full_size_properties_and_determinism():
     assert np.abs(W.sum(-1) - 1).max() < 1e-8 and W.min() > -1e-9
     turn = np.abs(np.diff(np.concatenate([wp[:, None], W], 1), axis=1)).sum(-1)
     assert turn.max() <= 0.2 + 1e-8
-    hold = np.log(np.exp(y.astype(np.float64)) @ wp[:, :, None])[..., 0].sum(-1)
+    hold = np.log(np.exp(y).astype(np.float64) @ wp[:, :, None])[..., 0].sum(-1)   # R in float32 (mpc.py:55)
     assert (val >= hold - 1e-9).all()
 
 
 def test_simplex_presolve_matches_ipm_and_oracle():
     """c = tau = 0, no short (BASELINE configs[1]): the closed-form presolve returns the IPM's
     optimum — the argmax vertex per period, the centre of the face on exact ties."""
-    import ctypes
     from koopman_mpc_portfolio_rebalancing_amd import _lib
     rng = np.random.default_rng(5)
     B, N, H = 64, 30, 5
@@ -146,14 +145,8 @@ def test_simplex_presolve_matches_ipm_and_oracle():
     assert np.allclose(W[1], 1.0 / N, rtol=0, atol=1e-15)
     for b in range(4):
         assert val[b] == pytest.approx(dense_ipm.reference_objective(W[b], wp[b], y[b], 0.0), abs=1e-12)
-    # the interior-point kernels (debug path 1) reach the same optimum
-    L = _lib.load()
-    L.kmpc_debug_solver_path.argtypes = [ctypes.c_int]
-    old = L.kmpc_debug_solver_path(1)
-    try:
-        Wi, sti, vali = _solve(wp, y, 0.0, 0.0)
-    finally:
-        L.kmpc_debug_solver_path(old)
+    # the interior-point kernels (per-call path KMPC_PATH_REGISTER: no presolve) reach the same optimum
+    Wi, sti, vali = _solve(wp, y, 0.0, 0.0, path=_lib.PATH_REGISTER)
     assert (sti == 0).all()
     # exact vs interior point stopped at mu 1e-9 (scaled): never worse, within the parity bar
     assert (val >= vali - 1e-12).all() and np.abs(val - vali).max() < 1e-7
@@ -192,3 +185,77 @@ def test_randomized_sweep_of_solver_paths():
             assert _feasible(W[b], wp[b], tau, short), (N, H, c, tau, short, b)
         if c > 0 and not short:
             assert np.abs(W[ok, 0] - Wo[ok, 0]).max() < 1e-3, (N, H, c, tau)
+
+
+def test_gross_returns_bit_exact():
+    """kmpc_gross_returns (the kernels' R = np.exp(yhat), kmpc_npexp.h) against numpy's float32 exp
+    on every 5th float32 bit pattern (859M inputs: all exponents, saturation, NaN / inf) and a
+    dense sweep of log-return-sized inputs."""
+    import ctypes
+    from koopman_mpc_portfolio_rebalancing_amd import _lib
+    L = _lib.load()
+    chunk = 1 << 26
+    for start in range(0, 1 << 32, chunk * 5):
+        n = min(chunk, ((1 << 32) - start + 4) // 5)
+        bits = torch.arange(start, start + 5 * n, 5, dtype=torch.int64, device="cuda").to(torch.int32)
+        x = bits.view(torch.float32)
+        R = torch.empty_like(x)
+        _lib.check(L.kmpc_gross_returns(n, x.data_ptr(), R.data_ptr(), None))
+        xh, Rh = x.cpu().numpy(), R.cpu().numpy()
+        with np.errstate(over="ignore", invalid="ignore"):
+            ref = np.exp(xh)
+        same = (Rh.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(Rh) & np.isnan(ref))
+        assert same.all(), (start, xh[~same][:4], Rh[~same][:4], ref[~same][:4])
+    x = torch.linspace(-0.3, 0.3, 1 << 24, device="cuda")
+    R = torch.empty_like(x)
+    _lib.check(L.kmpc_gross_returns(x.numel(), x.data_ptr(), R.data_ptr(), None))
+    assert np.array_equal(R.cpu().numpy().view(np.uint32), np.exp(x.cpu().numpy()).view(np.uint32))
+
+
+def test_float32_gross_return_ties():
+    """The program the reference solves sees R = np.exp(yhat) in float32 (mpc.py:55): distinct yhat
+    that round to one R are tied assets. Presolve (c = tau = 0): the face of the tied maximum, not
+    the argmax of yhat. Interior point with a cap: flat objective, centre w_prev (a float64
+    exp(yhat) would move to the cap, [0.6, 0.4]). Both against the oracle fed numpy's R."""
+    a = np.float32(0.01)
+    b = np.nextafter(a, np.float32(0))
+    c_ = np.nextafter(b, np.float32(0))
+    assert np.exp(np.array([a, b, c_]))[0] == np.exp(np.array([a, b, c_]))[2]
+    y = np.array([[[a, b, c_, 0.0]], [[0.0, b, 0.0, a]]], np.float32)          # [B=2, H=1, N=4]
+    wp = np.full((2, 4), 0.25)
+    W, st, val = _solve(wp, y, 0.0, 0.0)                                     # presolve
+    assert (st == 0).all()
+    assert np.array_equal(W[0, 0], [1 / 3, 1 / 3, 1 / 3, 0.0]) and np.array_equal(W[1, 0], [0.0, 0.5, 0.0, 0.5])
+    R = np.exp(y).astype(np.float64)
+    assert val[0] == pytest.approx(np.log(R[0, 0, 0]), abs=1e-15) and val[1] == np.log(R[1, 0, 1])
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y, 0.0, 0.0)
+    assert np.abs(val - valo).max() < 1e-12
+    y2 = np.array([[[a, b]]], np.float32)
+    W2, st2, val2 = _solve(np.array([[0.5, 0.5]]), y2, 0.0, 0.2)             # interior point, cap 0.2
+    Wo2, sto2, valo2, _ = oracle.solve_batch(np.array([[0.5, 0.5]]), y2, 0.0, 0.2)
+    assert st2[0] == 0 and sto2[0] == 0
+    assert np.abs(W2[0, 0] - 0.5).max() < 1e-6 and np.abs(Wo2[0, 0] - 0.5).max() < 1e-6
+    assert val2[0] == pytest.approx(np.log(np.float64(np.exp(a))), abs=1e-15)
+
+
+@pytest.mark.parametrize("N,H,B", [(30, 15, 1600), (300, 12, 1100)])
+def test_large_window_slot_reuse(N, H, B):
+    """The large-window kernel runs a persistent grid (768 / 512 workgroups) whose workgroups solve
+    window after window in the same workspace slab and LDS: with B past the slot count, windows
+    solved later by a reused workgroup must equal the same windows solved alone, bit for bit, and
+    a sample must match the oracle."""
+    rng = np.random.default_rng(N + H + B)
+    wp = rng.dirichlet(np.ones(N), B)
+    y = rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32)
+    W, st, val = _solve(wp, y, 1e-3, 0.3, full=False)
+    assert (st <= 1).all()
+    for b in (0, 767, 768, 1099, B - 1):
+        if b >= B:
+            continue
+        W1, st1, val1 = _solve(wp[b:b + 1], y[b:b + 1], 1e-3, 0.3, full=False)
+        assert st1[0] == st[b] and np.array_equal(W1[0], W[b]) and val1[0] == val[b], b
+    idx = np.array([1, 800, B - 2])
+    Wo, sto, valo, _ = oracle.solve_batch(wp[idx], y[idx], 1e-3, 0.3)
+    assert (sto <= 1).all()
+    assert np.abs(val[idx] - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
+    assert np.abs(W[idx] - Wo[:, 0]).max() < 1e-3

@@ -1,23 +1,20 @@
 """Dev probe: register kernels (path 1) vs the large-window kernel (path 2) on the same shapes,
-through the debug entry kmpc_debug_solver_path — the data behind kmpc_solve.hip's dispatch rule."""
+through the per-call kmpc_solve_desc.path — the data behind kmpc_solve.hip's dispatch rule."""
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from koopman_mpc_portfolio_rebalancing_amd import _lib, MPCConfig, solve_mpc_log_utility_batched
 L = _lib.load()
-L.kmpc_debug_solver_path.argtypes = [ctypes.c_int]
 
 def run(B, N, H, path):
     rng = np.random.default_rng(0)
     wp = torch.tensor(rng.dirichlet(np.ones(N), B), device="cuda")
     y = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device="cuda")
-    cfg = MPCConfig(horizon=H)
-    L.kmpc_debug_solver_path(path)
+    cfg = MPCConfig(horizon=H, solver_path=path)
     solve_mpc_log_utility_batched(wp[:64], y[:64], cfg); torch.cuda.synchronize()
     t = time.time()
     W, st, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
     torch.cuda.synchronize(); dt = time.time() - t
-    L.kmpc_debug_solver_path(0)
     return B / dt, v.cpu().numpy(), int((st.cpu().numpy() <= 1).sum())
 
 shapes = [(int(a), int(b)) for a, b in (s.split("x") for s in sys.argv[1:])] if len(sys.argv) > 1 else \
@@ -27,7 +24,6 @@ for N, H in shapes:
     try:
         r1, v1, ok1 = run(B, N, H, 1)
     except _lib.KmpcError as e:   # no register kernel for this shape
-        L.kmpc_debug_solver_path(0)
         print(f"N={N:4d} H={H:2d}: register path unsupported ({e})", flush=True)
         continue
     r2, v2, ok2 = run(B, N, H, 2)
