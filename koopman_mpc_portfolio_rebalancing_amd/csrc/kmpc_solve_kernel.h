@@ -89,8 +89,14 @@ struct PhaseClock {};
 #endif
 // refinement stops at ||r||_inf <= REFINE_RTOL ||b||_inf (the oracle uses the same rule)
 constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
-// corrector refinement only once the complementarity is this small (the oracle uses the same rule)
-constexpr double REFINE_MU = 1e-6;
+// corrector refinement only once the complementarity is this small (the oracle uses the same rule;
+// 1e-5 rather than 1e-6: with shorting allowed the w-block loses its barrier and the reduced system
+// is ill-conditioned one iteration earlier — an unrefined corrector at mu ~ 1.5e-6 left dual
+// residuals of 3e-6 and an optimal_inaccurate status in float64)
+#ifndef KMPC_REFINE_MU
+#define KMPC_REFINE_MU 1e-5
+#endif
+constexpr double REFINE_MU = KMPC_REFINE_MU;
 
 __host__ __device__ constexpr int pow2_at_least(int x) {
     int p = 1;
