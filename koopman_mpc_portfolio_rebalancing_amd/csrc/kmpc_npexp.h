@@ -24,9 +24,16 @@ __device__ __forceinline__ float np_expf(float x) {
     if (!(x == x)) return x;                                   // NaN in, NaN out
     if (x >= 88.72283935546875f) return __builtin_inff();      // overflow
     if (x <= -103.97208404541015625f) return 0.0f;             // underflow
-    // k = rint(x log2 e) by the 1.5·2^23 magic-number round (two float32 roundings, no FMA)
+    // k = rint(x log2 e) by the 1.5·2^23 magic-number round (two float32 roundings, no FMA). The
+    // empty asm statements pin each rounded intermediate: __fmul_rn / __fadd_rn are plain operators
+    // in a header outside this function's contract(off) scope, and the backend fused x·log2e + magic
+    // into one FMA there (k off by one on rare inputs, 1-2 ulp from numpy past x ~ 72, measured).
     const float magic = 0x1.8p+23f;
-    const float q = __fadd_rn(__fadd_rn(__fmul_rn(x, 1.442695040888963407359924681001892137f), magic), -magic);
+    float q = x * 1.442695040888963407359924681001892137f;
+    asm volatile("" : "+v"(q));
+    q = q + magic;
+    asm volatile("" : "+v"(q));
+    q = q - magic;
     // Cody-Waite reduction: r = x - k ln2 with ln2 split high / low (float32 FMAs)
     float r = __builtin_fmaf(q, -6.93145752e-1f, x);
     r = __builtin_fmaf(q, -1.42860677e-6f, r);
