@@ -78,7 +78,6 @@ extern "C" {
 #define KMPC_PATH_AUTO     0   /* kernel chosen by shape (and the closed-form presolve)            */
 #define KMPC_PATH_REGISTER 1   /* interior point in the register kernels where the shape fits them */
 #define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
-#define KMPC_PATH_PERIOD   3   /* interior point in the period-lane kernel (H N <= 1024, H <= 21)   */
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */

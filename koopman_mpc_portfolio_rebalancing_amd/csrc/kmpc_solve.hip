@@ -129,7 +129,7 @@ bool use_big(const SolveArgs& a) {
 size_t solve_workspace_bytes(const kmpc_solve_desc* d) {
     if (!d || d->B <= 0) return 0;
     const SolveArgs a = make_args(d);
-    if (simplex_case(a) || a.path == KMPC_PATH_PERIOD) return 0;
+    if (simplex_case(a)) return 0;
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_ws_bytes(a);
 #endif
@@ -148,7 +148,6 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
                            stream, a);
         return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
     }
-    if (a.path == KMPC_PATH_PERIOD) return pl_launch(a, stream);
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_launch(a, ws, ws_bytes, stream);
 #endif

@@ -28,8 +28,5 @@ int big_launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream)
 // constant-case kernels (kmpc_solve_h*_case.hip); KMPC_ERR_UNSUPPORTED if the case has none
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream);
-// period-lane kernel (kmpc_solve_pl.hip): H N <= 1024, H <= 21
-bool pl_supported(const SolveArgs& a);
-int pl_launch(const SolveArgs& a, hipStream_t stream);
 
 }  // namespace kmpc

@@ -262,33 +262,3 @@ def test_large_window_slot_reuse(N, H, B):
     assert (sto <= 1).all()
     assert np.abs(val[idx] - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
     assert np.abs(W[idx] - Wo[:, 0]).max() < 1e-3
-
-
-@pytest.mark.parametrize("N,H,c,tau,short", [(100, 10, 1e-3, 0.2, False), (10, 5, 1e-3, 0.2, False),
-                                             (30, 5, 0.0, 0.0, False), (1, 3, 1e-3, 0.3, False),
-                                             (64, 10, 1e-3, 0.5, False), (65, 7, 1e-3, 0.0, False),
-                                             (20, 4, 1e-2, 0.5, True), (40, 2, 0.0, 0.3, False),
-                                             (48, 21, 1e-3, 0.2, False), (1024, 1, 1e-3, 0.2, False),
-                                             (7, 12, 5e-3, 0.0, True), (3, 21, 1e-3, 0.2, False)])
-def test_period_lane_kernel_matches_oracle(N, H, c, tau, short):
-    """The period-lane kernel (kmpc_solve_pl.hip, one (t, i) pair per lane; forced through the
-    per-call path KMPC_PATH_PERIOD) against the long-double oracle: statuses, objective bar,
-    feasibility, W[0] where the optimum is unique; bit-identical on a relaunch."""
-    from koopman_mpc_portfolio_rebalancing_amd import _lib
-    rng = np.random.default_rng(N * 7 + H)
-    B = 5
-    wp = rng.dirichlet(np.ones(N), B)
-    if short:
-        wp = wp * 1.5 - 0.5 / N
-    y = rng.normal(5e-4, 0.02, (B, H, N)).astype(np.float32)
-    W, st, val = _solve(wp, y, c, tau, short, path=_lib.PATH_PERIOD)
-    W2, st2, val2 = _solve(wp, y, c, tau, short, path=_lib.PATH_PERIOD)
-    assert np.array_equal(W, W2) and np.array_equal(st, st2) and np.array_equal(val, val2, equal_nan=True)
-    Wo, sto, valo, _ = oracle.solve_batch(wp, y, c, tau, allow_short=short)
-    assert np.array_equal(st <= 1, sto <= 1), (st, sto)
-    ok = sto <= 1
-    assert np.abs(val[ok] - valo[ok]).max() <= 1e-6 + 1e-5 * np.abs(valo[ok]).max(), (val, valo)
-    for b in np.flatnonzero(ok):
-        assert _feasible(W[b], wp[b], tau, short), b
-    if c > 0 and not short:
-        assert np.abs(W[ok, 0] - Wo[ok, 0]).max() < 1e-3
