@@ -78,6 +78,8 @@ extern "C" {
 #define KMPC_PATH_AUTO     0   /* kernel chosen by shape (and the closed-form presolve)            */
 #define KMPC_PATH_REGISTER 1   /* interior point in the register kernels where the shape fits them */
 #define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
+#define KMPC_PATH_REGISTER_UNPACKED 3   /* register kernels, one window per wave even for N <= 32
+                                           (no lane-group packing); for A/B and tests             */
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */

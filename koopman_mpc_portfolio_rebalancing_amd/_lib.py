@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace
                     "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments", "kmpc_solve_mv_ws",
                     "kmpc_mv_workspace_bytes", "kmpc_gross_returns")
 
-PATH_AUTO, PATH_REGISTER, PATH_LARGE = 0, 1, 2   # kmpc_solve_desc.path
+PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
 
 
 class KmpcError(RuntimeError):

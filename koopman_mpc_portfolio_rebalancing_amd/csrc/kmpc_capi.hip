@@ -16,7 +16,7 @@ int check_solve(const kmpc_solve_desc* d) {
     if (d->H > 21) return KMPC_ERR_UNSUPPORTED;   // Schur system (3H) must fit one wavefront
     // c < 0 makes -c ||dw||_1 concave in the maximization: not DCP, cvxpy raises (mpc.py:66-103)
     if (d->cost_coeff < 0.0) return KMPC_ERR_INVALID;
-    if (d->path < KMPC_PATH_AUTO || d->path > KMPC_PATH_LARGE) return KMPC_ERR_INVALID;
+    if (d->path < KMPC_PATH_AUTO || d->path > KMPC_PATH_REGISTER_UNPACKED) return KMPC_ERR_INVALID;
     return KMPC_OK;
 }
 

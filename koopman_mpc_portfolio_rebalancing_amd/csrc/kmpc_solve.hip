@@ -18,7 +18,8 @@ namespace {
 
 // per-call solver path (kmpc_solve_desc.path): KMPC_PATH_AUTO by shape, KMPC_PATH_REGISTER =
 // interior point in the register kernels whenever they support the shape (no presolve),
-// KMPC_PATH_LARGE = the large-window kernel
+// KMPC_PATH_LARGE = the large-window kernel, KMPC_PATH_REGISTER_UNPACKED = the register kernels
+// with one window per wave even for small windows (no lane-group packing, no presolve)
 bool simplex_case(const SolveArgs& a) {
     return a.path == KMPC_PATH_AUTO && !(a.c > 0.0) && !(a.tau > 0.0) && !a.allow_short;
 }
@@ -115,7 +116,7 @@ bool use_big(const SolveArgs& a) {
 #ifdef KMPC_DEV_ONLY_H10
     return false;
 #else
-    if (a.path == KMPC_PATH_REGISTER) return false;
+    if (a.path == KMPC_PATH_REGISTER || a.path == KMPC_PATH_REGISTER_UNPACKED) return false;
     if (a.path == KMPC_PATH_LARGE) return true;
     // measured on MI355X (tools/path_ab.py): the register kernels win up to 256 assets at
     // H <= 10 (N = 192: 76k vs 41k windows/s); the large-window kernel wins past 10 periods at any
@@ -151,6 +152,14 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_launch(a, ws, ws_bytes, stream);
 #endif
+    // N <= 32: several windows per wave on lane groups (16 lanes for N <= 16 at H <= 5, else 32)
+    if (a.path != KMPC_PATH_REGISTER_UNPACKED && a.N <= 32 && a.H <= 10) {
+#ifndef KMPC_DEV_ONLY_H10
+        const int rc = a.H <= 2 ? launch_ipm_packed<2>(a, stream)
+                                : (a.H <= 5 ? launch_ipm_packed<5>(a, stream) : launch_ipm_packed<10>(a, stream));
+        if (rc != KMPC_ERR_UNSUPPORTED) return rc;
+#endif
+    }
     // H == 5 / 10 with N <= 128 in the two common constraint cases: constant-case kernels
     if (a.H == 10 || a.H == 5) {
         const int rc = a.H == 10 ? launch_ipm_case<10>(a, stream) :

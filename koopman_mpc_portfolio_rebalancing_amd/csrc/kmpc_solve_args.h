@@ -28,5 +28,9 @@ int big_launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream)
 // constant-case kernels (kmpc_solve_h*_case.hip); KMPC_ERR_UNSUPPORTED if the case has none
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream);
+// packed small-window kernels, 64 / GL windows per wave (kmpc_solve_p*.hip); KMPC_ERR_UNSUPPORTED
+// outside N <= 32, 3 H <= 32
+template <int HM>
+int launch_ipm_packed(const SolveArgs& a, hipStream_t stream);
 
 }  // namespace kmpc

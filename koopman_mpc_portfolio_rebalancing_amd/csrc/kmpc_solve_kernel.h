@@ -221,6 +221,85 @@ __device__ __forceinline__ double bcast(double v, int src) {
     return as_f64(__builtin_amdgcn_readlane(x.x, src), __builtin_amdgcn_readlane(x.y, src));
 }
 
+// ---- lane groups ---------------------------------------------------------------------------------
+// GL lanes per window. GL = 64: a window owns whole waves (64 ceil(N / 64) threads). GL = 16 / 32:
+// small windows (N <= GL, 3 H <= GL) packed 4 / 2 per wave, each on its own 16-lane DPP rows, so
+// every cross-lane step stays inside the group: the butterfly levels below GL, and the broadcast
+// of a group lane by DPP row_newbcast (+ one permlane16 swap for 32-lane groups) instead of
+// v_readlane. The group index picks the window; gvt is the thread's index inside its window.
+template <int GL>
+__device__ __forceinline__ int gvt() { return GL == 64 ? (int)threadIdx.x : (int)(threadIdx.x & (GL - 1)); }
+template <int GL>
+__device__ __forceinline__ int grp() { return GL == 64 ? 0 : (int)(threadIdx.x / GL); }
+template <int GL>   // lane within the wave's share of the window / wave index within the window
+__device__ __forceinline__ int glane() { return (int)(threadIdx.x & ((GL == 64 ? WAVE : GL) - 1)); }
+template <int GL>
+__device__ __forceinline__ int gwave() { return GL == 64 ? (int)(threadIdx.x / WAVE) : 0; }
+
+template <int GL>
+__device__ __forceinline__ double group_sum(double v) {
+    if constexpr (GL > 32) v = pair_sum<32>(v);
+    if constexpr (GL > 16) v = pair_sum<16>(v);
+    v = pair_sum<8>(v); v = pair_sum<4>(v); v = pair_sum<2>(v); v = pair_sum<1>(v);
+    return v;
+}
+template <int GL>
+__device__ __forceinline__ double group_max(double v) {
+    if constexpr (GL > 32) v = fmax(v, partner<32>(v));
+    if constexpr (GL > 16) v = fmax(v, partner<16>(v));
+    v = fmax(v, partner<8>(v)); v = fmax(v, partner<4>(v)); v = fmax(v, partner<2>(v)); v = fmax(v, partner<1>(v));
+    return v;
+}
+template <int GL>
+__device__ __forceinline__ double group_min(double v) {
+    if constexpr (GL > 32) v = fmin(v, partner<32>(v));
+    if constexpr (GL > 16) v = fmin(v, partner<16>(v));
+    v = fmin(v, partner<8>(v)); v = fmin(v, partner<4>(v)); v = fmin(v, partner<2>(v)); v = fmin(v, partner<1>(v));
+    return v;
+}
+template <int C>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int2 x = as_i2(v);
+    return as_f64(__builtin_amdgcn_update_dpp(0, x.x, C, 0xf, 0xf, false),
+                  __builtin_amdgcn_update_dpp(0, x.y, C, 0xf, 0xf, false));
+}
+// lane j of every 16-lane row to the whole row (DPP row_newbcast:j). j is a constant in every
+// (unrolled) caller, so the switch folds to one DPP move per dword.
+__device__ __forceinline__ double row_bcast(double v, int j) {
+    switch (j & 15) {
+        case 0: return dpp_f64<0x150>(v);
+        case 1: return dpp_f64<0x151>(v);
+        case 2: return dpp_f64<0x152>(v);
+        case 3: return dpp_f64<0x153>(v);
+        case 4: return dpp_f64<0x154>(v);
+        case 5: return dpp_f64<0x155>(v);
+        case 6: return dpp_f64<0x156>(v);
+        case 7: return dpp_f64<0x157>(v);
+        case 8: return dpp_f64<0x158>(v);
+        case 9: return dpp_f64<0x159>(v);
+        case 10: return dpp_f64<0x15a>(v);
+        case 11: return dpp_f64<0x15b>(v);
+        case 12: return dpp_f64<0x15c>(v);
+        case 13: return dpp_f64<0x15d>(v);
+        case 14: return dpp_f64<0x15e>(v);
+        default: return dpp_f64<0x15f>(v);
+    }
+}
+// group lane `src` to every lane of its group
+template <int GL>
+__device__ __forceinline__ double gbcast(double v, int src) {
+    if constexpr (GL == 64) {
+        return bcast(v, src);
+    } else if constexpr (GL == 16) {
+        return row_bcast(v, src);
+    } else {
+        static_assert(GL == 32, "lane group of 16, 32 or 64");
+        double a = row_bcast(v, src), b = a;
+        swap16(a, b);   // a: the even row's value in both rows of a 32-lane half, b: the odd row's
+        return (src & 16) ? b : a;
+    }
+}
+
 // one butterfly level of the reduce-scatter: pairs (v[j], v[j+h]), j < h
 template <int M, int D>
 __device__ __forceinline__ void rs_level(double (&v)[M], int& n, int& slot) {
@@ -252,11 +331,13 @@ __device__ __forceinline__ void rs_level(double (&v)[M], int& n, int& slot) {
 // Wave reduce-scatter of M = 2^k values (k <= 6): afterwards v[0] of lane l holds the wave total
 // of slot `slot` (returned); the 64/M lanes that agree in their high bits share a slot. Each
 // level sends the half it does not keep: ~M exchanges instead of 6M.
-template <int M>
+// GL < 64: over the lanes of a group (M <= GL).
+template <int M, int GL = 64>
 __device__ __forceinline__ int wave_reduce_scatter(double (&v)[M]) {
+    static_assert(M <= GL, "one slot per lane at most");
     int slot = 0, n = M;
-    rs_level<M, 32>(v, n, slot);
-    rs_level<M, 16>(v, n, slot);
+    if constexpr (GL > 32) rs_level<M, 32>(v, n, slot);
+    if constexpr (GL > 16) rs_level<M, 16>(v, n, slot);
     rs_level<M, 8>(v, n, slot);
     rs_level<M, 4>(v, n, slot);
     rs_level<M, 2>(v, n, slot);
@@ -342,11 +423,12 @@ struct Case<-1> {
 };
 __host__ __device__ constexpr int case_of(bool hw, bool hs, bool ht) { return (hw ? 1 : 0) | (hs ? 2 : 0) | (ht ? 4 : 0); }
 
-template <int HM, int MAXT, int FL = -1, int CS = MAXT, bool QL = false>
+template <int HM, int MAXT, int FL = -1, int CS = MAXT, bool QL = false, int GL = 64>
 struct Thread : Case<FL> {
     using Case<FL>::hw;
     using Case<FL>::hs;
     using Case<FL>::ht;
+    static constexpr int GLN = GL;   // lanes per window (lane groups)
     static constexpr bool L = cold_in_lds<HM, MAXT, CS, QL>();
     int H, N, i;
     bool act;
@@ -428,7 +510,7 @@ struct Thread : Case<FL> {
 };
 
 // Block reductions over the workgroup with a double-buffered slot array (one barrier each).
-template <int HM, int NWM>
+template <int HM, int NWM, int GL = 64>
 struct Reducer {
     Shared<HM, NWM>& sh;
     int nw;
@@ -439,11 +521,11 @@ struct Reducer {
     // per-wave slots, threads j < M total slot j over the waves (fixed order: deterministic)
     template <int M>
     __device__ __forceinline__ void sum(double (&v)[M]) {
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        const int slot = wave_reduce_scatter<M>(v);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        const int slot = wave_reduce_scatter<M, GL>(v);
         double* r = &sh.red[buf][0][0];
         constexpr int RW = Shared<HM, NWM>::RW;
-        if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
+        if ((lane & ((GL / M) - 1)) == 0) r[wv * RW + slot] = v[0];
         __syncthreads();
         // the slot reads (uniform-address broadcasts) in flight together, in groups of <= 16
         // doubles per lane, then the sums
@@ -478,7 +560,7 @@ struct Reducer {
     }
     __device__ __forceinline__ void periods(double (&a)[HM], double (&b)[HM]) {
         constexpr int M = pow2_at_least(2 * HM);
-        if constexpr (M <= 64) {
+        if constexpr (M <= GL) {
             double v[M];
 #pragma unroll
             for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : 0.0);
@@ -492,7 +574,7 @@ struct Reducer {
     }
     __device__ __forceinline__ void periods(double (&a)[HM], double (&b)[HM], double (&c)[HM]) {
         constexpr int M = pow2_at_least(3 * HM);
-        if constexpr (M <= 64) {
+        if constexpr (M <= GL) {
             double v[M];
 #pragma unroll
             for (int t = 0; t < M; ++t)
@@ -511,15 +593,15 @@ struct Reducer {
     // HM per-period threads).
     template <int M, int NA>
     __device__ __forceinline__ void own_slots(double (&v)[M], double (&out)[NA]) {
-        static_assert(NA * HM <= M && M <= 64, "slots");
+        static_assert(NA * HM <= M && M <= GL, "slots");
         constexpr int RW = Shared<HM, NWM>::RW;
         static_assert(RW >= M, "reduction row");
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        const int slot = wave_reduce_scatter<M>(v);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        const int slot = wave_reduce_scatter<M, GL>(v);
         double* r = &sh.red[buf][0][0];
-        if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
+        if ((lane & ((GL / M) - 1)) == 0) r[wv * RW + slot] = v[0];
         __syncthreads();
-        const int t = threadIdx.x < HM ? threadIdx.x : 0;
+        const int t = gvt<GL>() < HM ? gvt<GL>() : 0;
         double tmp[NWM][NA];
 #pragma unroll
         for (int q = 0; q < NWM; ++q)
@@ -546,7 +628,7 @@ struct Reducer {
     __device__ __forceinline__ void own3(const double (&a)[HM], const double (&b)[HM], const double (&c)[HM],
                                          double (&out)[4]) {
         constexpr int M = pow2_at_least(3 * HM);
-        static_assert(M <= 64, "own3");
+        static_assert(M <= GL, "own3");
         double v[M], o[3];
 #pragma unroll
         for (int t = 0; t < M; ++t)
@@ -554,43 +636,20 @@ struct Reducer {
         own_slots<M, 3>(v, o);
         out[0] = o[0]; out[1] = o[1]; out[2] = o[2]; out[3] = 0.0;
     }
-    // four [HM] arrays (two reductions when 4 HM > 64)
-    __device__ __forceinline__ void own4(const double (&a)[HM], const double (&b)[HM], const double (&c)[HM],
-                                         const double (&d)[HM], double (&out)[4]) {
-        constexpr int M4 = pow2_at_least(4 * HM);
-        if constexpr (M4 <= 64) {
-            double v[M4];
-#pragma unroll
-            for (int t = 0; t < M4; ++t)
-                v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : (t < 3 * HM ? c[t - 2 * HM] : (t < 4 * HM ? d[t - 3 * HM] : 0.0)));
-            own_slots<M4, 4>(v, out);
-        } else {
-            constexpr int M2 = pow2_at_least(2 * HM);
-            double v[M2], o[2];
-#pragma unroll
-            for (int t = 0; t < M2; ++t) v[t] = t < HM ? a[t] : (t < 2 * HM ? b[t - HM] : 0.0);
-            own_slots<M2, 2>(v, o);
-            out[0] = o[0]; out[1] = o[1];
-#pragma unroll
-            for (int t = 0; t < M2; ++t) v[t] = t < HM ? c[t] : (t < 2 * HM ? d[t - HM] : 0.0);
-            own_slots<M2, 2>(v, o);
-            out[2] = o[0]; out[3] = o[1];
-        }
-    }
     // per-period sums of a (in place), the block minimum of mn and the block sums of two scalars
     // (slots HM, HM + 1 of the same reduce-scatter), sharing one barrier
     __device__ __forceinline__ double periods_min_sums(double (&a)[HM], double mn, double& s1, double& s2) {
         constexpr int M = pow2_at_least(HM + 2);
         constexpr int RW = Shared<HM, NWM>::RW;
         static_assert(RW > M, "a spare reduction slot per wave");
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+        const int lane = glane<GL>(), wv = gwave<GL>();
         double v[M];
 #pragma unroll
         for (int t = 0; t < M; ++t) v[t] = t < HM ? a[t] : (t == HM ? s1 : (t == HM + 1 ? s2 : 0.0));
-        const int slot = wave_reduce_scatter<M>(v);
-        mn = wave_min(mn);
+        const int slot = wave_reduce_scatter<M, GL>(v);
+        mn = group_min<GL>(mn);
         double* r = &sh.red[buf][0][0];
-        if ((lane & ((WAVE / M) - 1)) == 0) r[wv * RW + slot] = v[0];
+        if ((lane & ((GL / M) - 1)) == 0) r[wv * RW + slot] = v[0];
         if (lane == 0) r[wv * RW + M] = mn;
         __syncthreads();
         double t0[NWM][HM + 3];
@@ -621,9 +680,9 @@ struct Reducer {
     // block sum of s and block maximum of mx, sharing one barrier
     __device__ __forceinline__ void sum_max(double s, double mx, double& S, double& MX) {
         constexpr int RW = Shared<HM, NWM>::RW;
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        s = wave_sum(s);
-        mx = wave_max(mx);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        s = group_sum<GL>(s);
+        mx = group_max<GL>(mx);
         double* r = &sh.red[buf][0][0];
         if (lane == 0) { r[wv * RW] = s; r[wv * RW + 1] = mx; }
         __syncthreads();
@@ -643,8 +702,8 @@ struct Reducer {
         buf ^= Shared<HM, NWM>::NB - 1;
     }
     __device__ __forceinline__ double sum1(double x) {
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        x = wave_sum(x);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        x = group_sum<GL>(x);
         double* r = &sh.red[buf][0][0];
         constexpr int RW = Shared<HM, NWM>::RW;
         if (lane == 0) r[wv * RW] = x;
@@ -657,8 +716,8 @@ struct Reducer {
         return s;
     }
     __device__ __forceinline__ double max1(double x) {
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        x = wave_max(x);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        x = group_max<GL>(x);
         double* r = &sh.red[buf][0][0];
         constexpr int RW = Shared<HM, NWM>::RW;
         if (lane == 0) r[wv * RW] = x;
@@ -671,8 +730,8 @@ struct Reducer {
         return s;
     }
     __device__ __forceinline__ double min1(double x) {
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-        x = wave_min(x);
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        x = group_min<GL>(x);
         double* r = &sh.red[buf][0][0];
         constexpr int RW = Shared<HM, NWM>::RW;
         if (lane == 0) r[wv * RW] = x;
@@ -716,7 +775,7 @@ __device__ __forceinline__ void dual_residual(const TH& T, const Shared<HM, NWM>
 // sh.lb5, sh.lb6), in place: on return bw = dw, bs = ds (and q in sh.bs; the budget multipliers
 // are q[2H..3H)). In-place arrays keep the register footprint of the solve to four [HM] arrays.
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+__device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
                                        double (&bw)[HM], double (&bs)[HM], bool with_c) {
     constexpr int KM = 3 * HM;
     const int H = T.H;
@@ -753,7 +812,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
         // three chunks (a, v, budget columns) of MP = pow2(HM) slots, one barrier
         constexpr int MP = pow2_at_least(HM);
         constexpr int RW = Shared<HM, NWM>::RW;
-        const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+        const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
         double* rb = &sh.red[R.buf][0][0];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -768,14 +827,14 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
                 }
                 v[t] = val;
             }
-            const int slot = wave_reduce_scatter<MP>(v);
-            if ((lane & ((WAVE / MP) - 1)) == 0) rb[wv * RW + k * MP + slot] = v[0];
+            const int slot = wave_reduce_scatter<MP, TH::GLN>(v);
+            if ((lane & ((TH::GLN / MP) - 1)) == 0) rb[wv * RW + k * MP + slot] = v[0];
         }
         __syncthreads();
         R.buf ^= Shared<HM, NWM>::NB - 1;
         KMPC_PH(lp, 9);
         // wave 0: q = G^{-1} (bs - [0; 0; b6]) by forward / back substitution; lane r owns row r
-        if (threadIdx.x < WAVE) {
+        if (gvt<TH::GLN>() < WAVE) {
             double rhs = 0.0;
             if (lane < KM) {
                 const int k = lane / HM, t = lane % HM;
@@ -797,7 +856,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
                 const double gd = sh.gid[lr];
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = 0; j < KM - 1; ++j) rhs = fma(-lf[j], bcast(rhs, j), rhs);
+                for (int j = 0; j < KM - 1; ++j) rhs = fma(-lf[j], gbcast<TH::GLN>(rhs, j), rhs);
                 rhs *= gd;   // D^{-1}
             }
             // backward: L^T q = D^{-1} y (lane r uses column r of L: row-major L, contiguous)
@@ -807,7 +866,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
                 for (int j = 1; j < KM; ++j) lb[j - 1] = sh.G[j * KM + lr];
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = KM - 1; j > 0; --j) rhs = fma(-lb[j - 1], bcast(rhs, j), rhs);
+                for (int j = KM - 1; j > 0; --j) rhs = fma(-lb[j - 1], gbcast<TH::GLN>(rhs, j), rhs);
             }
             if (lane < KM) sh.bs[lane] = rhs;
         }
@@ -864,7 +923,7 @@ __device__ __forceinline__ void newton_rows(const TH& T, Shared<HM, NWM>& sh, in
 // the unreduced system (one lsolve body for the solve and its refinements).
 // On exit: T.dw, T.ds, sh.dnu, sh.dz4, sh.dl4.
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+__device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
                                        int n_refine) {
     const int H = T.H;
     PhaseClock np;
@@ -885,7 +944,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                 bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
                                    fmax(fabs(T.rc1[t]), fmax(fabs(T.rc2[t]), fabs(T.rc3[t])))));
         }
-        if (threadIdx.x == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
+        if (gvt<TH::GLN>() == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     }
     if (n_refine > 0) bn = R.max1(bn);
     KMPC_PH(np, 12);
@@ -901,11 +960,11 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         if (r == 0) {
 #pragma unroll
             for (int t = 0; t < HM; ++t) { T.dw[t] = r0[t]; T.ds[t] = r1[t]; }
-            if (threadIdx.x < HM) sh.dnu[threadIdx.x] = (int)threadIdx.x < H ? sh.bs[2 * HM + threadIdx.x] : 0.0;
+            if (gvt<TH::GLN>() < HM) sh.dnu[gvt<TH::GLN>()] = (int)gvt<TH::GLN>() < H ? sh.bs[2 * HM + gvt<TH::GLN>()] : 0.0;
         } else {
 #pragma unroll
             for (int t = 0; t < HM; ++t) { T.dw[t] += r0[t]; T.ds[t] += r1[t]; }
-            if (threadIdx.x < HM) sh.dnu[threadIdx.x] += (int)threadIdx.x < H ? sh.bs[2 * HM + threadIdx.x] : 0.0;
+            if (gvt<TH::GLN>() < HM) sh.dnu[gvt<TH::GLN>()] += (int)gvt<TH::GLN>() < H ? sh.bs[2 * HM + gvt<TH::GLN>()] : 0.0;
         }
         KMPC_PH(np, 13);
         if (r >= n_refine) break;
@@ -936,15 +995,15 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                 r0[t] = r1[t] = 0.0;
             }
             rn = fmax(rn, fmax(fabs(r0[t]), fabs(r1[t])));
-            if (threadIdx.x == 0 && t < H) rn = fmax(rn, fabs(sh.b6[t] - sdw[t]));
+            if (gvt<TH::GLN>() == 0 && t < H) rn = fmax(rn, fabs(sh.b6[t] - sdw[t]));
             nl2 = (t < H) ? dl2 : 0.0;
             nl3 = (t < H) ? dl3 : 0.0;
         }
         rn = R.max1(rn);
         KMPC_PH(np, 14);
         if (rn <= REFINE_RTOL * bn) break;
-        if (threadIdx.x < HM) {
-            const int t = threadIdx.x;
+        if (gvt<TH::GLN>() < HM) {
+            const int t = gvt<TH::GLN>();
             sh.lb5[t] = 0.0;                                   // row (6) residual is identically 0
             sh.lb6[t] = (t < H) ? sh.b6[t] - sdw[t] : 0.0;
         }
@@ -958,8 +1017,8 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #pragma unroll
     for (int t = 0; t < HM; ++t) sds[t] = (T.act && t < H) ? T.ds[t] : 0.0;
     const double st_own = R.own1(sds);
-    if (threadIdx.x < HM) {
-        const int t = threadIdx.x;
+    if (gvt<TH::GLN>() < HM) {
+        const int t = gvt<TH::GLN>();
         const double st = st_own;
         const bool on = T.ht && t < H;
         sh.dz4[t] = on ? -st + sh.rg4[t] : 0.0;
@@ -974,7 +1033,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 // c0 + a c1 + a^2 c2 (c0 is the residual phase's mu sum): block-summed in spare slots of the same
 // reduction, so the Mehrotra centring needs no pass or barrier of its own.
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+__device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
                                            double& c1, double& c2) {
     const int H = T.H;
     double a = 1e300, mdw[HM];
@@ -1010,8 +1069,8 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
     }
     if (qx > 0.0) a = fmin(a, rcp_nr(qx));
     // the cap slack / multiplier bounds of period t on its owner lane (folded into the block min)
-    if (T.ht && (int)threadIdx.x < H) {
-        const int t = threadIdx.x;
+    if (T.ht && (int)gvt<TH::GLN>() < H) {
+        const int t = gvt<TH::GLN>();
         a = to_bound(sh.z4[t], sh.dz4[t], a);
         a = to_bound(sh.l4[t], sh.dl4[t], a);
     }
@@ -1031,7 +1090,7 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
 // with c = alpha_t (a), eps_t (v), 1 (budget); Q^{-1} columns from the LDL^T:
 //   Qi[c][c] = dq_c,  Qi[r][c] = Lr_{r+1} Qi[r+1][c]  (r < c).
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM>& R,
+__device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
                                       PhaseClock& ph) {
     constexpr int KM = 3 * HM;
     constexpr int MC = Shared<HM, NWM>::MC;
@@ -1060,8 +1119,8 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         T.iz3.set(t, iz3);
     }
     const double st_own = R.own1(sp);
-    if (threadIdx.x < HM) {
-        const int t = threadIdx.x;
+    if (gvt<TH::GLN>() < HM) {
+        const int t = gvt<TH::GLN>();
         const double st = st_own;
         const double ga = (T.ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
         sh.rho[t] = (T.ht && t < H) ? ga / (1.0 + ga * st) : 0.0;
@@ -1109,7 +1168,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     // column coefficients of this asset: alpha_t (a), eps_t (v)
     auto al = [&](int t) -> double { return (T.act && t < H) ? T.m[t] * sh.iden[t] * T.irsig : 0.0; };
     auto ep = [&](int t) -> double { return (T.act && t < H && T.ht) ? sh.sr[t] * T.bma(t) * T.P[t] : 0.0; };
-    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
     if constexpr (static_gram<HM, NWM>()) {
         // Static-slot Gram: every entry (j, l) of G with period(j) <= period(l) = c has a
         // compile-time slot (gram_slot_jl). Each lane puts its contribution for slot s in
@@ -1157,8 +1216,8 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                         if constexpr (slot % CH == CH - 1 || slot == NS - 1) {
 #pragma unroll
                             for (int z = slot % CH + 1; z < CH; ++z) buf[z] = 0.0;
-                            const int s = (slot - slot % CH) + wave_reduce_scatter<CH>(buf);
-                            if ((lane & (WAVE / CH - 1)) == 0 && s < NS) sh.gred[wv * NS + s] = buf[0];
+                            const int s = (slot - slot % CH) + wave_reduce_scatter<CH, TH::GLN>(buf);
+                            if ((lane & (TH::GLN / CH - 1)) == 0 && s < NS) sh.gred[wv * NS + s] = buf[0];
                         }
                     }
                 });
@@ -1168,11 +1227,11 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         });
         __syncthreads();
         // assemble both triangles of G: read the partials, barrier (gred aliases G), write
-        constexpr int SPT = (NS + WAVE - 1) / WAVE;
+        constexpr int SPT = (NS + TH::GLN - 1) / TH::GLN;
         double tot[SPT];
 #pragma unroll
         for (int k = 0; k < SPT; ++k) {
-            const int s = threadIdx.x + k * blockDim.x;
+            const int s = gvt<TH::GLN>() + k * (TH::GLN == 64 ? (int)blockDim.x : TH::GLN);
             double v = 0.0;
             if (s < NS)
                 for (int w = 0; w < R.nw; ++w) v += sh.gred[w * NS + s];
@@ -1181,7 +1240,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SPT; ++k) {
-            const int s = threadIdx.x + k * blockDim.x;
+            const int s = gvt<TH::GLN>() + k * (TH::GLN == 64 ? (int)blockDim.x : TH::GLN);
             if (s < NS) {
                 int j, l;
                 gram_slot_jl<HM>(s, j, l);
@@ -1238,11 +1297,11 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                     }
                     v[q] = x;
                 }
-                const int slot = wave_reduce_scatter<MC>(v);
-                if ((lane & ((WAVE / MC) - 1)) == 0) rb[wv * RW + k * MC + slot] = v[0];
+                const int slot = wave_reduce_scatter<MC, TH::GLN>(v);
+                if ((lane & ((TH::GLN / MC) - 1)) == 0) rb[wv * RW + k * MC + slot] = v[0];
             }
             __syncthreads();
-            for (int q = threadIdx.x; q < 3 * MC; q += blockDim.x) {
+            for (int q = gvt<TH::GLN>(); q < 3 * MC; q += (TH::GLN == 64 ? (int)blockDim.x : TH::GLN)) {
                 const int tyl = q / MC, j = q % MC;
                 if (j < KM) {
                     const int tyj = j / HM, tj = j % HM;
@@ -1269,7 +1328,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     // I' adds 1 on the a- and v-type diagonals. L is stored strictly lower (zero elsewhere).
     // (the column broadcast of the LDL^T steps uses reduction slots: no reduction is in flight here)
     double* col = &sh.red[0][0][0];
-    if (threadIdx.x < WAVE) {
+    if (gvt<TH::GLN>() < WAVE) {
         const int r = lane;
         const bool rused = r < KM && (r % HM) < H && (r / HM != 1 || T.ht);
         double g[KM];
@@ -1294,7 +1353,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #pragma unroll
                 for (int k = j + 1; k < KM; ++k) cv[k] = col[k];
             }
-            const double d = bcast(u, j);
+            const double d = gbcast<TH::GLN>(u, j);
             bad = bad || !(d > 0.0) || !(d < 1e300);
             // 1 / d: v_rcp_f64 + two Newton steps (~1 ulp)
             const double dm = fmax(d, 1e-300);
@@ -1329,7 +1388,7 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 // Write the current iterate as the answer (W[0] or W) and return problem.value at it:
 // sum_t log(w_t . exp(y_t)) - c sum_t ||w_t - w_{t-1}||_1  (mpc.py:66-103).
 template <int HM, int NWM, class TH>
-__device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM>& R, double* wout,
+__device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM, TH::GLN>& R, double* wout,
                                               const float* yh, double c, int tw) {
     const int H = T.H, N = T.N;
     double rw[HM], l1n[HM];
@@ -1351,19 +1410,24 @@ __device__ __forceinline__ double record_best(const TH& T, Reducer<HM, NWM>& R, 
 }
 
 // EXACT: H == HM known at compile time (all period predicates fold away).
-template <int HM, int MAXT, bool EXACT, int FL = -1, int CS = MAXT, bool QL = false>
+// GL < 64: 64 / GL windows packed per one-wave block (lane groups; MAXT = 64, N <= GL).
+template <int HM, int MAXT, bool EXACT, int FL = -1, int CS = MAXT, bool QL = false, int GL = 64>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <= KMPC_WPE2_HM ? 2 : 1))) ipm_kernel(SolveArgs args) {
-    static_assert(3 * HM <= WAVE, "Schur system must fit one wave");
+    static_assert(3 * HM <= GL, "Schur system must fit one lane group");
+    static_assert(GL == 64 || MAXT == 64, "lane groups pack one-wave blocks");
     constexpr int NWM = MAXT / WAVE;
-    __shared__ Shared<HM, NWM> sh;
-    const int b = blockIdx.x;
-    const int nw = blockDim.x / WAVE;
-    Reducer<HM, NWM> R(sh, nw);
-    Thread<HM, MAXT, FL, CS, QL> T;
+    constexpr int WPB = GL == 64 ? 1 : 64 / GL;   // windows per block
+    __shared__ Shared<HM, NWM> shv[WPB];
+    auto& sh = shv[grp<GL>()];
+    const int b = blockIdx.x * WPB + grp<GL>();
+    if (b >= args.B) return;   // (whole groups of the last block)
+    const int nw = GL == 64 ? (int)(blockDim.x / WAVE) : 1;
+    Reducer<HM, NWM, GL> R(sh, nw);
+    Thread<HM, MAXT, FL, CS, QL, GL> T;
     T.bind_cold();
     T.H = EXACT ? HM : args.H;
     T.N = args.N;
-    T.i = threadIdx.x;
+    T.i = gvt<GL>();
     T.act = T.i < args.N;
     T.set_case(!args.allow_short, (args.c > 0.0) || (args.tau > 0.0), args.tau > 0.0);
     T.tau = args.tau;
@@ -1440,8 +1504,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 T.l2[t] = T.l3[t] = (on && T.hs) ? 1.0 : 0.0;
             }
             const double st0 = R.own1(ss0);
-            if (threadIdx.x < HM) {
-                const int t = threadIdx.x;
+            if (gvt<GL>() < HM) {
+                const int t = gvt<GL>();
                 const double st = st0;
                 sh.z4[t] = (T.ht && t < H) ? fmax(T.tau - st, 0.5 * T.tau) : 1.0;
                 sh.l4[t] = (T.ht && t < H) ? 1.0 : 0.0;
@@ -1474,8 +1538,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     R.own3(mw, sw, ssum, o);
 #pragma unroll
                     for (int t = 0; t < HM; ++t) l1_own[t] = l1n[t];
-                    if (threadIdx.x < HM) {
-                        const int t = threadIdx.x;
+                    if (gvt<GL>() < HM) {
+                        const int t = gvt<GL>();
                         const double a = o[0], b2 = o[1], c2 = o[2];
                         my_rw = b2 + a;          // sum_i exp(yhat) w = sum w + sum expm1(yhat) w
                         const bool on = t < H;
@@ -1514,7 +1578,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 mu *= inv_ncon;
                 const double merit = fmax(mu, fmax(rd, pr));
                 min_pr = fmin(min_pr, pr);
-                if (args.trace && b == 0 && threadIdx.x == 0) {
+                if (args.trace && b == 0 && gvt<GL>() == 0) {
                     args.trace[4 * it + 0] = mu; args.trace[4 * it + 1] = rd; args.trace[4 * it + 2] = pr;
                 }
                 if (!domain_ok || !isfinite(merit)) break;
@@ -1526,9 +1590,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     for (int t = 0; t < HM; ++t)
                         if (T.act && t < H && t < tw) wout[t * N + T.i] = T.w[t];
                     const double l1t = R.own1(l1_own);
-                    if (threadIdx.x < HM) {
-                        sh.best_rw[threadIdx.x] = my_rw;
-                        sh.best_l1[threadIdx.x] = l1t;
+                    if (gvt<GL>() < HM) {
+                        sh.best_rw[gvt<GL>()] = my_rw;
+                        sh.best_l1[gvt<GL>()] = l1t;
                     }
                     best_obj = 0.0;
                 } else if (best < 1e-6 && merit > 1e4 * best) {
@@ -1596,14 +1660,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                             }
                         }
                     }
-                    if (threadIdx.x < HM && T.ht && (int)threadIdx.x < H) {
-                        const int t = threadIdx.x;
+                    if (gvt<GL>() < HM && T.ht && (int)gvt<GL>() < H) {
+                        const int t = gvt<GL>();
                         sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
                     }
-                    if (threadIdx.x < HM) newton_rows<HM, NWM>(T, sh, threadIdx.x);   // the corrector's rows
+                    if (gvt<GL>() < HM) newton_rows<HM, NWM>(T, sh, gvt<GL>());   // the corrector's rows
                     __syncthreads();
                 }
-                if (args.trace && b == 0 && threadIdx.x == 0) args.trace[4 * it + 3] = step;
+                if (args.trace && b == 0 && gvt<GL>() == 0) args.trace[4 * it + 3] = step;
                 KMPC_PH(ph, 5);
                 // ---- update ----
                 {
@@ -1629,8 +1693,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 // period threads overwrite them; the next reads (period owners, then everyone) sit
                 // behind the next iteration's residual barriers
                 __syncthreads();
-                if (threadIdx.x < HM && (int)threadIdx.x < H) {
-                    const int t = threadIdx.x;
+                if (gvt<GL>() < HM && (int)gvt<GL>() < H) {
+                    const int t = gvt<GL>();
                     sh.z4[t] += step * sh.dz4[t];
                     sh.l4[t] += step * sh.dl4[t];
                     sh.nu[t] += step * sh.dnu[t];
@@ -1658,17 +1722,18 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
         for (int t = 0; t < HM; ++t)
             if (t < tw) wout[t * N + T.i] = T.wpi;
     }
-    if (threadIdx.x == 0) {
+    if (gvt<GL>() == 0) {
         args.obj[b] = ok ? best_obj : __builtin_nan("");
         args.status[b] = status;
         if (args.iters) args.iters[b] = it;
     }
 }
 
-template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false>
+template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false, int GL = 64>
 int launch_one(const SolveArgs& a, int nt, hipStream_t stream) {
     const size_t lds = cold_bytes<HM, MAXT, CS, QL>();
-    hipLaunchKernelGGL((ipm_kernel<HM, MAXT, EXACT, FL, CS, QL>), dim3(a.B), dim3(nt), lds, stream, a);
+    constexpr int WPB = GL == 64 ? 1 : 64 / GL;
+    hipLaunchKernelGGL((ipm_kernel<HM, MAXT, EXACT, FL, CS, QL, GL>), dim3((a.B + WPB - 1) / WPB), dim3(nt), lds, stream, a);
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 
@@ -1717,6 +1782,34 @@ int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
     }
     if (nt > 128) return KMPC_ERR_UNSUPPORTED;
     if (fl == 1) return nt <= 64 ? launch_one<HM, 64, true, 1>(a, nt, stream) : launch_one<HM, 128, true, 1>(a, nt, stream);
+    return KMPC_ERR_UNSUPPORTED;
+}
+
+}  // namespace kmpc
+
+namespace kmpc {
+
+// Packed launcher: windows of N <= 32 assets (3 H <= GL) run 64 / GL per one-wave block, each on
+// its own lane group (GL = 16 for N <= 16 when 3 HM <= 16, else 32). Constant-case kernels for
+// H == HM in the two common cases (FL = 7, FL = 1), the generic kernel otherwise. Returns
+// KMPC_ERR_UNSUPPORTED outside that range (the caller then uses one window per wave).
+template <int HM>
+int launch_ipm_packed(const SolveArgs& a, hipStream_t stream) {
+    if (a.H > HM || a.N > 32 || 3 * HM > 32) return KMPC_ERR_UNSUPPORTED;
+    const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
+    const bool exact = a.H == HM;
+    if constexpr (3 * HM <= 16) {
+        if (a.N <= 16) {
+            if (exact && fl == 7) return launch_one<HM, 64, true, 7, 64, false, 16>(a, 64, stream);
+            if (exact && fl == 1) return launch_one<HM, 64, true, 1, 64, false, 16>(a, 64, stream);
+            return launch_one<HM, 64, false, -1, 64, false, 16>(a, 64, stream);
+        }
+    }
+    if constexpr (3 * HM <= 32) {
+        if (exact && fl == 7) return launch_one<HM, 64, true, 7, 64, false, 32>(a, 64, stream);
+        if (exact && fl == 1) return launch_one<HM, 64, true, 1, 64, false, 32>(a, 64, stream);
+        return launch_one<HM, 64, false, -1, 64, false, 32>(a, 64, stream);
+    }
     return KMPC_ERR_UNSUPPORTED;
 }
 

@@ -34,7 +34,7 @@ class MPCConfig:
     max_iter: int = 80
     tol: float = 1e-9
     n_refine: int = 0  # 0 -> kernel default
-    solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM
+    solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM, 3 register IPM without lane-group packing
 
 
 def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:

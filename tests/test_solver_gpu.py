@@ -111,6 +111,47 @@ def test_ragged_shapes_match_oracle(N, H):
     assert np.abs(W[:, 0] - Wo[:, 0]).max() < 1e-3
 
 
+@pytest.mark.parametrize("N,H,case", [(10, 5, 0), (16, 5, 1), (1, 3, 0), (13, 4, 2), (3, 2, 3),   # 16-lane groups
+                                      (17, 5, 0), (30, 5, 1), (32, 10, 0), (20, 7, 2), (25, 10, 3),  # 32-lane groups
+                                      (31, 1, 0), (10, 5, 4)])
+def test_packed_small_windows_match_oracle(N, H, case):
+    """N <= 32: 4 (16-lane groups: N <= 16, H <= 5) or 2 (32-lane groups) windows per wave. A batch
+    that does not fill the last wave, a non-finite and an infeasible window between solved ones
+    (their groups leave the iteration early while their neighbours keep iterating), against the
+    long-double oracle and the one-window-per-wave kernels (KMPC_PATH_REGISTER_UNPACKED)."""
+    from koopman_mpc_portfolio_rebalancing_amd import _lib
+    c, tau, short = [(1e-3, 0.2, False), (0.0, 0.0, False), (1e-3, 0.0, False), (0.0, 0.3, False),
+                     (5e-3, 0.0, True)][case]
+    rng = np.random.default_rng(100 * N + H + case)
+    B = 11
+    wp = rng.dirichlet(np.ones(N), B)
+    if short:
+        wp = wp * 1.5 - 0.5 / N
+    y = rng.normal(5e-4, 0.02, (B, H, N)).astype(np.float32)
+    y[4, H - 1, 0] = np.nan                     # solver_error inside a pack
+    if tau > 0 and N > 1:
+        wp[6] = 0.0
+        wp[6, 0] = 3.0                          # sum(w_prev) = 3: the cap makes the budget unreachable
+    path = _lib.PATH_REGISTER if (c == 0.0 and tau == 0.0 and not short) else 0   # (no presolve)
+    W, st, val = _solve(wp, y, c, tau, short, path=path)
+    W2, st2, val2 = _solve(wp, y, c, tau, short, path=path)
+    assert np.array_equal(W, W2) and np.array_equal(st, st2) and np.array_equal(val, val2, equal_nan=True)
+    Wu, stu, valu = _solve(wp, y, c, tau, short, path=_lib.PATH_REGISTER_UNPACKED)
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y, c, tau, allow_short=short)
+    assert np.array_equal(st <= 1, sto <= 1) and np.array_equal(st <= 1, stu <= 1), (st, sto, stu)
+    assert st[4] == 4 and np.array_equal(W[4], np.tile(wp[4], (H, 1))) and np.isnan(val[4])
+    if tau > 0 and N > 1:
+        assert st[6] == 2 and np.array_equal(W[6], np.tile(wp[6], (H, 1)))
+    ok = sto <= 1
+    assert ok.sum() >= 8
+    bar = 1e-6 + 1e-5 * np.abs(valo[ok]).max()
+    assert np.abs(val[ok] - valo[ok]).max() <= bar and np.abs(val[ok] - valu[ok]).max() <= bar
+    for b in np.flatnonzero(ok):
+        assert _feasible(W[b], wp[b], tau, short), b
+    if c > 0 and not short:
+        assert np.abs(W[ok, 0] - Wo[ok, 0]).max() < 1e-3
+
+
 def test_full_size_properties_and_determinism():
     """cfg3 shape at 8192 windows: every window optimal and feasible, never worse than holding
     (W = tile(w_prev) is feasible), bit-identical on a second launch."""

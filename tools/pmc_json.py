@@ -1,10 +1,13 @@
 """Per-window PMC figures of the solve kernel for bench.py's roofline ``traffic`` and the f64 VALU
-roofline: python tools/pmc_json.py OUT.json WINDOWS_PER_LAUNCH FETCH_DB WRITE_DB [F64_DB]
+utilisation: python tools/pmc_json.py OUT.json WINDOWS_PER_LAUNCH ASSETS BLOCK FETCH_DB WRITE_DB F64_DB [F64_PEAK_LOG]
 
 FETCH_SIZE is doubled (gfx950 correction, MI355X_MICROARCH.md §HBM); sizes are in KB per dispatch.
-Executed f64 FLOPs = 64 lanes x (ADD + MUL + TRANS + 2 FMA) wave-instructions per dispatch.
+Executed f64 FLOPs = 64 lanes x (ADD + MUL + TRANS + 2 FMA) wave-instructions per dispatch; the
+active-lane fraction is ASSETS / BLOCK (the window's lanes that hold an asset). F64_PEAK_LOG is the
+output of tools/dev/f64_peak (the f64 FMA rate measured on the same part).
 """
 import json
+import re
 import sqlite3
 import sys
 
@@ -19,17 +22,39 @@ def mean(db, counter):
     return float(r[0]) if r and r[0] is not None else None
 
 
-out, B, fetch_db, write_db = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
-d = {"kernel": "ipm_kernel<10,128,true,7> (kmpc_solve, constant-case)", "windows_per_launch": B,
+def kernel_name(db):
+    con = sqlite3.connect(db)
+    try:
+        r = con.execute("select kernel_name from counters_collection where kernel_name like '%ipm_kernel%' "
+                        "limit 1").fetchone()
+    finally:
+        con.close()
+    return r[0] if r else None
+
+
+out, B, N, blk = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+fetch_db, write_db, f64_db = sys.argv[5], sys.argv[6], sys.argv[7]
+d = {"kernel": kernel_name(fetch_db), "windows_per_launch": B,
      "fetch_bytes_per_window": 2 * 1024 * mean(fetch_db, "FETCH_SIZE") / B,
      "write_bytes_per_window": 1024 * mean(write_db, "WRITE_SIZE") / B,
      "source": "rocprofv3 --pmc passes of `python bench.py --cpu-seconds 0 --steps 3 --warmup 1` (tools/gpu_round.sh)"}
-if len(sys.argv) > 5:
-    f = sys.argv[5]
-    ins = {c: mean(f, c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
-                                   "SQ_INSTS_VALU_TRANS_F64")}
-    if all(v is not None for v in ins.values()):
-        d["f64_flops_per_window"] = 64 * (ins["SQ_INSTS_VALU_ADD_F64"] + ins["SQ_INSTS_VALU_MUL_F64"] +
-                                          ins["SQ_INSTS_VALU_TRANS_F64"] + 2 * ins["SQ_INSTS_VALU_FMA_F64"]) / B
+ins = {c: mean(f64_db, c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                    "SQ_INSTS_VALU_TRANS_F64", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+                                    "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU")}
+if all(ins[c] is not None for c in list(ins)[:4]):
+    d["f64_flops_per_window"] = 64 * (ins["SQ_INSTS_VALU_ADD_F64"] + ins["SQ_INSTS_VALU_MUL_F64"] +
+                                      ins["SQ_INSTS_VALU_TRANS_F64"] + 2 * ins["SQ_INSTS_VALU_FMA_F64"]) / B
+    d["active_lane_fraction"] = N / blk
+if ins["SQ_WAVE_CYCLES"]:
+    d["wait_any_fraction"] = ins["SQ_WAIT_ANY"] / ins["SQ_WAVE_CYCLES"]
+    d["valu_active_fraction"] = ins["SQ_ACTIVE_INST_VALU"] / ins["SQ_WAVE_CYCLES"]
+if ins["SQ_INSTS_VALU"]:
+    d["f64_share_of_valu_insts"] = sum(ins[c] for c in list(ins)[:4]) / ins["SQ_INSTS_VALU"]
+d["raw_counters_per_dispatch"] = ins
+if len(sys.argv) > 8:
+    m = re.search(r"f64 fma: .*?([\d.]+) TFLOP/s", open(sys.argv[8]).read())
+    if m:
+        d["f64_peak_flops"] = float(m.group(1)) * 1e12
+        d["f64_peak_source"] = "measured: tools/dev/f64_peak (dependent-free v_fma_f64 stream over every CU)"
 json.dump(d, open(out, "w"), indent=1)
 print(json.dumps(d))

@@ -33,15 +33,19 @@ def main():
         seen.add(r[0])
         lines.append("| `" + r[0][:60] + "` | " + " | ".join(str(x) for x in r[1:]) + " |")
     for db in pmcs:
-        lines += ["", f"## PMC ({db})", "", "| kernel | counter | dispatches | mean value (KB) | corrected bytes / dispatch |",
+        lines += ["", f"## PMC ({db})", "", "| kernel | counter | dispatches | mean value per dispatch | corrected bytes / dispatch |",
                   "|---|---|---|---|---|"]
         q = ("select kernel_name, counter_name, count(*), avg(value) from counters_collection "
              "group by kernel_name, counter_name")
         for name, ctr, n, v in rows(db, q):
             if name.startswith("void at::") or name.startswith("__amd"):
                 continue
-            corr = v * 1024 * (2 if ctr == "FETCH_SIZE" else 1)
-            lines.append(f"| `{name[:60]}` | {ctr} | {n} | {v:.1f} | {corr:.4g} |")
+            if ctr in ("FETCH_SIZE", "WRITE_SIZE"):   # KB; FETCH_SIZE x2 on gfx950
+                corr = f"{v * 1024 * (2 if ctr == 'FETCH_SIZE' else 1):.4g}"
+                val = f"{v:.1f} KB"
+            else:
+                corr, val = "", f"{v:.4g}"
+            lines.append(f"| `{name[:60]}` | {ctr} | {n} | {val} | {corr} |")
     open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
