@@ -44,7 +44,7 @@ HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 # per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
-PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02_solve_pmc.json")
+PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_solve_pmc.json")
 
 
 def parse():

@@ -979,7 +979,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         if (sh.flag) break;
         double step = 0.0, smu = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
-            ph_newton(W, (pass == 0 || mu > REFINE_MU) ? 0 : a.n_refine, pass == 1, smu);
+            ph_newton(W, (pass == 0 || mu > (W.hw() ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : a.n_refine, pass == 1, smu);
             double cc1, cc2;
             const double amax = ph_step(W, cc1, cc2);
             if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }

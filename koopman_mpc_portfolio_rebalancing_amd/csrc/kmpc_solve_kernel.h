@@ -89,14 +89,19 @@ struct PhaseClock {};
 #endif
 // refinement stops at ||r||_inf <= REFINE_RTOL ||b||_inf (the oracle uses the same rule)
 constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
-// corrector refinement only once the complementarity is this small (the oracle uses the same rule;
-// 1e-5 rather than 1e-6: with shorting allowed the w-block loses its barrier and the reduced system
-// is ill-conditioned one iteration earlier — an unrefined corrector at mu ~ 1.5e-6 left dual
-// residuals of 3e-6 and an optimal_inaccurate status in float64)
+// corrector refinement only once the complementarity is this small (the oracle uses the same rule):
+// 1e-6, and 1e-5 with shorting allowed — there the w-block has no barrier and the reduced system
+// is ill-conditioned one iteration earlier (an unrefined corrector at mu ~ 1.5e-6 left dual
+// residuals of 3e-6 and an optimal_inaccurate status in float64). Without shorting 1e-5 only adds
+// refinement passes (C3 solve -3%, measured r03).
 #ifndef KMPC_REFINE_MU
-#define KMPC_REFINE_MU 1e-5
+#define KMPC_REFINE_MU 1e-6
+#endif
+#ifndef KMPC_REFINE_MU_SHORT
+#define KMPC_REFINE_MU_SHORT 1e-5
 #endif
 constexpr double REFINE_MU = KMPC_REFINE_MU;
+constexpr double REFINE_MU_SHORT = KMPC_REFINE_MU_SHORT;
 
 __host__ __device__ constexpr int pow2_at_least(int x) {
     int p = 1;
@@ -374,12 +379,20 @@ struct Cold<HM, CS, true> {
 __host__ __device__ constexpr int n_cold(bool ql) { return ql ? 8 : 6; }
 // cold arrays go to LDS when they fit next to the static LDS (G, its transpose, reduction slots)
 // within one CU's 160 KB; otherwise (HM = 21, or 1024-thread blocks) they stay in registers.
-template <int HM, int MAXT, int CS, bool QL>
+// Packed kernels of the no-short-only case (FL = 1, no turnover terms: ~24 dwords spilled with the
+// cold arrays in registers) keep them in registers: 13.4 instead of 28.8 KB of LDS per block,
+// eight waves per CU instead of five — N = 10, H = 5: 34 -> 50 M windows/s (measured r03); the
+// turnover case spills ~190 dwords that way (13.4 -> 9.3 M windows/s) and keeps them in LDS.
+#ifndef KMPC_PACKED_COLD_REG   // dev A/B: every packed kernel's cold arrays in registers
+#define KMPC_PACKED_COLD_REG 0
+#endif
+template <int HM, int MAXT, int CS, bool QL, int GL = 64, int FL = -1>
 constexpr bool cold_in_lds() {
+    if (GL < 64 && (KMPC_PACKED_COLD_REG || FL == 1)) return false;
     return MAXT <= 256 && (n_cold(QL) * HM * CS + 9 * HM * HM) * 8 + 16 * 1024 <= 160 * 1024;
 }
-template <int HM, int MAXT, int CS, bool QL>
-constexpr size_t cold_bytes() { return cold_in_lds<HM, MAXT, CS, QL>() ? sizeof(double) * n_cold(QL) * HM * CS : 0; }
+template <int HM, int MAXT, int CS, bool QL, int GL = 64, int FL = -1>
+constexpr size_t cold_bytes() { return cold_in_lds<HM, MAXT, CS, QL, GL, FL>() ? sizeof(double) * n_cold(QL) * HM * CS : 0; }
 
 // ---- shared state -------------------------------------------------------------------------------
 
@@ -429,7 +442,7 @@ struct Thread : Case<FL> {
     using Case<FL>::hs;
     using Case<FL>::ht;
     static constexpr int GLN = GL;   // lanes per window (lane groups)
-    static constexpr bool L = cold_in_lds<HM, MAXT, CS, QL>();
+    static constexpr bool L = cold_in_lds<HM, MAXT, CS, QL, GL, FL>();
     int H, N, i;
     bool act;
     double c, tau, sig, isig, irsig, wpi;
@@ -1619,7 +1632,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 double step = 0.0;
                 for (int pass = 0; pass < 2; ++pass) {
                     // predictor unrefined (it only sets the step estimate, sigma and the
-                    // second-order term); corrector refined adaptively once mu <= REFINE_MU
+                    // second-order term); corrector refined adaptively once mu <= REFINE_MU (_SHORT)
                     // (before that G is well conditioned and the IPM self-corrects) — as the oracle
                     // w and s are not read by the Newton solve: park them in scratch across it
                     // (plain stores; one batch of loads after), so that their 40 VGPRs serve the
@@ -1631,7 +1644,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { park[t] = T.w[t]; park[HM + t] = T.s[t]; }
                     asm volatile("" :: "v"(&park[0]) : "memory");
-                    newton<HM, NWM>(T, sh, R, (pass == 0 || mu > REFINE_MU) ? 0 : args.n_refine);
+                    newton<HM, NWM>(T, sh, R, (pass == 0 || mu > (T.hw ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : args.n_refine);
                     asm volatile("" :: "v"(&park[0]) : "memory");
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { T.w[t] = park[t]; T.s[t] = park[HM + t]; }
@@ -1731,7 +1744,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
 
 template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false, int GL = 64>
 int launch_one(const SolveArgs& a, int nt, hipStream_t stream) {
-    const size_t lds = cold_bytes<HM, MAXT, CS, QL>();
+    const size_t lds = cold_bytes<HM, MAXT, CS, QL, GL, FL>();
     constexpr int WPB = GL == 64 ? 1 : 64 / GL;
     hipLaunchKernelGGL((ipm_kernel<HM, MAXT, EXACT, FL, CS, QL, GL>), dim3((a.B + WPB - 1) / WPB), dim3(nt), lds, stream, a);
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;

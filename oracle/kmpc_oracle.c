@@ -641,11 +641,13 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
                 }
                 if (W.ht) W.rc4[t] += W.dz4[t] * W.dl4[t] - sg * mu;
             }
-            {   /* corrector refinement only once mu <= REFINE_MU (the kernel's REFINE_MU) */
+            {   /* corrector refinement only once mu <= 1e-6, 1e-5 with shorting (the kernels'
+                   REFINE_MU / REFINE_MU_SHORT) */
                 static double refine_mu = -1;
-                if (refine_mu < 0) refine_mu = getenv("KMPC_ORACLE_REFINE_MU") ? atof(getenv("KMPC_ORACLE_REFINE_MU")) : 1e-5;
+                if (refine_mu < 0) refine_mu = getenv("KMPC_ORACLE_REFINE_MU") ? atof(getenv("KMPC_ORACLE_REFINE_MU")) : 0;
+                const double rmu = refine_mu > 0 ? refine_mu : (W.hw ? 1e-6 : 1e-5);
                 const int nr = W.n_refine;
-                if (mu > (real)refine_mu) W.n_refine = 0;
+                if (mu > (real)rmu) W.n_refine = 0;
                 newton(&W);
                 W.n_refine = nr;
             }

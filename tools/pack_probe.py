@@ -5,6 +5,9 @@ import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from koopman_mpc_portfolio_rebalancing_amd import _lib, MPCConfig, solve_mpc_log_utility_batched
+if os.environ.get("KMPC_DEV_LIB"):   # a variant library (csrc/Makefile pvar)
+    _lib._lib = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["KMPC_DEV_LIB"]))
+ONLY = os.environ.get("PACKED_ONLY") == "1"
 
 CASES = {"c": dict(cost_coeff=1e-3, max_turnover=0.2), "n": dict(cost_coeff=0.0, max_turnover=0.0),
          "s": dict(cost_coeff=1e-3, max_turnover=0.0, allow_short=True)}
@@ -34,6 +37,10 @@ for a in args:
     B = 262144 if N * H <= 100 else 131072
     p = 1 if case == "n" else 0
     r1, W1, s1, v1, i1 = run(B, N, H, case, p)
+    if ONLY:
+        print(f"N={N:3d} H={H:2d} {case}: packed {r1 / 1e6:6.2f} M/s ({i1.mean():5.2f} it, {(s1 == 0).mean():.4f} opt)",
+              flush=True)
+        continue
     r0, W0, s0, v0, i0 = run(B, N, H, case, _lib.PATH_REGISTER_UNPACKED)
     ok = (s1 <= 1) & (s0 <= 1)
     print(f"N={N:3d} H={H:2d} {case}: packed {r1 / 1e6:6.2f} M/s ({i1.mean():5.2f} it, {(s1 == 0).mean():.4f} opt)  "

@@ -52,9 +52,9 @@ if ins["SQ_INSTS_VALU"]:
     d["f64_share_of_valu_insts"] = sum(ins[c] for c in list(ins)[:4]) / ins["SQ_INSTS_VALU"]
 d["raw_counters_per_dispatch"] = ins
 if len(sys.argv) > 8:
-    m = re.search(r"f64 fma: .*?([\d.]+) TFLOP/s", open(sys.argv[8]).read())
-    if m:
-        d["f64_peak_flops"] = float(m.group(1)) * 1e12
-        d["f64_peak_source"] = "measured: tools/dev/f64_peak (dependent-free v_fma_f64 stream over every CU)"
+    v = [float(x) for x in re.findall(r"f64 fma: .*?([\d.]+) TFLOP/s", open(sys.argv[8]).read())]
+    if v:   # best of the probe's runs (the first one includes clock ramp-up)
+        d["f64_peak_flops"] = max(v) * 1e12
+        d["f64_peak_source"] = "measured: tools/dev/f64_peak, best of its runs (independent v_fma_f64 chains over every CU)"
 json.dump(d, open(out, "w"), indent=1)
 print(json.dumps(d))
