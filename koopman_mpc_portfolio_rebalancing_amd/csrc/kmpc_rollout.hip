@@ -45,6 +45,8 @@ struct GemmArgs {
     float thr;
     const float* mean; const float* stdv;   // EPI_DESTD [N]
     int bf16;                     // 1: operands rounded to bf16, v_mfma_f32_32x32x16_bf16 (fp32 accumulate)
+    int ksplit;                   // > 1: blockIdx.z takes a K slice, raw partials to part[z][M][N]
+    float* part;                  //      (splitk_epilogue_kernel sums them in slice order, then the epilogue)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -68,6 +70,21 @@ __device__ __forceinline__ float destandardize(float y, float sd, float mu) {
 #pragma clang fp contract(off)
     const float p = y * sd;
     return p + mu;
+}
+
+// the epilogue of one output element
+__device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, float acc) {
+    float v = acc + (g.bias ? g.bias[n] : 0.0f);
+    if (g.epi == EPI_ACT) {
+        v = apply_act(v, g.act);
+    } else if (g.epi == EPI_SHRINK) {
+        v += g.R[(size_t)m * g.ldr + n];
+        const float av = fabsf(v) - g.thr;
+        v = (av > 0.0f) ? copysignf(av, v) : 0.0f * v;
+    } else if (g.epi == EPI_DESTD) {
+        v = destandardize(v, g.stdv[n], g.mean[n]);
+    }
+    return v;
 }
 
 // fused epilogue of a WT x WT block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D
@@ -134,6 +151,13 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
 
     const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
                         ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
+    // split K: slice blockIdx.z of ksplit (whole BK tiles)
+    int kbeg = 0, kend = g.K;
+    if (g.ksplit > 1) {
+        const int kc = ((g.K + g.ksplit * BK - 1) / (g.ksplit * BK)) * BK;
+        kbeg = blockIdx.z * kc;
+        kend = min(g.K, kbeg + kc);
+    }
     // A and B tiles: TM rows x 32 k = 8 TM float4 per operand, TM / 32 per thread. The next
     // k-tile's global loads are issued into registers before this tile's MFMAs (register double
     // buffering: one LDS buffer, the HBM / L2 latency under the math).
@@ -148,13 +172,13 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
             va[q] = f32x4{0.f, 0.f, 0.f, 0.f};
             vb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
             const int ma = m0 + row, nb = n0 + row;
-            if (vec_ok && kk + 3 < g.K) {
+            if (vec_ok && kk + 3 < kend) {
                 if (ma < g.M) va[q] = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
                 if (nb < g.N) vb[q] = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (kk + e < g.K) {
+                    if (kk + e < kend) {
                         if (ma < g.M) va[q][e] = g.A[(size_t)ma * g.lda + kk + e];
                         if (nb < g.N) vb[q][e] = g.B[(size_t)nb * g.ldb + kk + e];
                     }
@@ -162,8 +186,8 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
             }
         }
     };
-    fetch(0);
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
+    fetch(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
             const int idx = tid + q * 256;
@@ -172,7 +196,7 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
             *(f32x4*)(Bs + row * LDS_STRIDE + c4) = vb[q];
         }
         __syncthreads();
-        if (k0 + BK < g.K) fetch(k0 + BK);
+        if (k0 + BK < kend) fetch(k0 + BK);
         const int r = lane & 31, h = lane >> 5;
         float af[WT][16], bf[WT][16];
 #pragma unroll
@@ -196,7 +220,33 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         __syncthreads();
     }
+    if (g.ksplit > 1) {   // raw partial of this K slice
+        float* P = g.part + (size_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+        for (int a = 0; a < WT; ++a)
+#pragma unroll
+            for (int b = 0; b < WT; ++b) {
+                const int n = n0 + wn + b * 32 + (lane & 31);
+                if (n >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < g.M) P[(size_t)m * g.N + n] = acc[a][b][r];
+                }
+            }
+        return;
+    }
     epilogue<WT>(g, acc, m0, n0, wm, wn, lane);
+}
+
+// split-K: C = epi(sum of the ksplit partials, in slice order)
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmArgs g) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)g.M * g.N) return;
+    const int m = (int)(i / g.N), n = (int)(i % g.N);
+    float v = g.part[i];
+    for (int z = 1; z < g.ksplit; ++z) v += g.part[(size_t)z * g.M * g.N + i];
+    g.C[(size_t)m * g.ldc + n] = epi_value(g, m, n, v);
 }
 
 // bf16 variant (BASELINE configs[4]: "bf16 MFMA rollout"): the same 128 x 128 tile and epilogues;
@@ -422,6 +472,80 @@ __global__ void __launch_bounds__(256) latent_steps_kernel(LatentArgs a) {
     }
 }
 
+// Small window batches (fewer than 8,192 windows: 32-row blocks would leave CUs idle, BASELINE
+// configs[1] has 4,096 -> 128 blocks): the same H-step loop with 16 windows per block on
+// v_mfma_f32_16x16x4_f32 (A[l&15][k], B[k][l&15], k = 4 (l>>4) + e over a 16-k chunk; C/D
+// col = l&15, row = 4 (l>>4) + i). z <- z K: L / 16 column tiles over the 4 waves; decode: the
+// ceil(N / 16) decoder row tiles. One accumulator per tile (exact fp32, the k order of a chunk is
+// the same for both operands).
+constexpr int LAT16 = 16;
+__device__ __forceinline__ void tile_dot16(const float* As, int lda, const float* Bg, int L, bool brow_ok, int lane,
+                                           f32x4& acc) {
+    const int r = lane & 15, kq = lane >> 4;
+    const float* pa = As + r * lda + 4 * kq;
+    const float* pb = Bg + (size_t)r * L + 4 * kq;
+    f32x4 bn = brow_ok ? *(const f32x4*)pb : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < L; k0 += 16) {
+        const f32x4 av = *(const f32x4*)(pa + k0);
+        const f32x4 bv = bn;
+        if (k0 + 16 < L) bn = brow_ok ? *(const f32x4*)(pb + k0 + 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
+    }
+}
+
+__global__ void __launch_bounds__(256) latent_steps16_kernel(LatentArgs a) {
+    extern __shared__ float zs[];   // [2][16][L + 4]
+    const int L = a.L, LS = L + 4, N = a.N;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int m0 = blockIdx.x * LAT16;
+    float* zc = zs;
+    float* zn = zs + LAT16 * LS;
+    for (int idx = tid; idx < LAT16 * L; idx += 256) {
+        const int row = idx / L, col = idx - row * L;
+        zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
+    }
+    __syncthreads();
+    const int nct = L / 16, ndt = (N + 15) / 16;
+    const int c = lane & 15, rq = 4 * (lane >> 4);
+    for (int k = 0; k < a.H; ++k) {
+        for (int ct = wv; ct < nct; ct += 4) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            tile_dot16(zc, LS, a.Kt + (size_t)ct * 16 * L, L, true, lane, acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) zn[(rq + i) * LS + ct * 16 + c] = acc[i];
+        }
+        __syncthreads();
+        if (a.ball) {   // x / ||x||_2 per row: 16 threads per row
+            const int row = tid >> 4, part = tid & 15;
+            float sq = 0.0f;
+            for (int j = part; j < L; j += 16) sq += zn[row * LS + j] * zn[row * LS + j];
+            sq += __shfl_xor(sq, 1, 64);
+            sq += __shfl_xor(sq, 2, 64);
+            sq += __shfl_xor(sq, 4, 64);
+            sq += __shfl_xor(sq, 8, 64);
+            const float nrm = sqrtf(sq);
+            for (int j = part; j < L; j += 16) zn[row * LS + j] = zn[row * LS + j] / nrm;
+            __syncthreads();
+        }
+        for (int ct = wv; ct < ndt; ct += 4) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            const int nrow = ct * 16 + c;
+            tile_dot16(zn, LS, a.D + (size_t)ct * 16 * L, L, nrow < N, lane, acc);
+            if (nrow < N) {
+                const float bias = a.bias ? a.bias[nrow] : 0.0f, mu = a.mean[nrow], sd = a.stdv[nrow];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = m0 + rq + i;
+                    if (m < a.B) a.yhat[((size_t)m * a.H + k) * N + nrow] = destandardize(acc[i] + bias, sd, mu);
+                }
+            }
+        }
+        float* t = zc; zc = zn; zn = t;
+        __syncthreads();
+    }
+}
+
 // the fused H-step kernel: fp32, one decoder layer, L % 32 == 0 and <= 512 (2 x 32 rows of z in
 // LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
 // descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
@@ -431,13 +555,30 @@ static bool latent_fusable(const kmpc_rollout_desc* d) {
            !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn != KMPC_NORM_ID && d->norm_fn != KMPC_NORM_BALL);
 }
 
-static int gemm(const GemmArgs& g, hipStream_t s) {
+// split-K partial buffer: SPLITK slices of at most SPLITK_ELEMS outputs (split only when the
+// 64 x 64 tiles number fewer than 256, i.e. M N <= 256 * 64 * 64)
+constexpr int SPLITK = 4;
+constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
+
+static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
+    g.ksplit = 1;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     if (g.bf16) {
         hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
     } else if ((size_t)grid.x * grid.y < 512) {
         dim3 grid64((g.N + 63) / 64, (g.M + 63) / 64);
+        // fewer 64 x 64 tiles than CUs (e.g. the 128-wide last encoder layer of BASELINE configs[1]:
+        // 4,096 x 128 -> 128 tiles) with a long K: split K in SPLITK slices (4 x the workgroups), the
+        // partials summed in slice order by the epilogue kernel (deterministic)
+        if (part && (size_t)grid64.x * grid64.y < 256 && g.K >= 128 * SPLITK) {
+            g.ksplit = SPLITK;
+            g.part = part;
+            hipLaunchKernelGGL(gemm_nt_kernel<1>, dim3(grid64.x, grid64.y, SPLITK), dim3(256), 0, s, g);
+            const size_t n = (size_t)g.M * g.N;
+            hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+            return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+        }
         hipLaunchKernelGGL(gemm_nt_kernel<1>, grid64, dim3(256), 0, s, g);
     } else {
         hipLaunchKernelGGL(gemm_nt_kernel<2>, grid, dim3(256), 0, s, g);
@@ -473,6 +614,8 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
     bytes += align256(sizeof(float) * (size_t)d->L * d->L);        // S^T (LISTA)
     bytes += 2 * align256(sizeof(float) * B * wmax);               // ping-pong activations
     bytes += 2 * align256(sizeof(float) * B * d->L);               // z, c (LISTA) / z next
+    const size_t part = B * (size_t)wmax < SPLITK_ELEMS ? B * (size_t)wmax : SPLITK_ELEMS;
+    bytes += align256(sizeof(float) * SPLITK * part);              // split-K partials (small batches)
     return bytes;
 }
 
@@ -480,7 +623,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
 // layer, written with row stride ldo); ping/pong are [B, wmax] scratch buffers.
 static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* out, int ldo,
                    int last_cols, int last_epi, const float* mean, const float* stdv, float* ping,
-                   float* pong, int wmax, int bf16, hipStream_t s) {
+                   float* pong, int wmax, int bf16, hipStream_t s, float* part) {
     const float* cur = X;
     int ldc = ldx;
     for (int l = 0; l < m.n_layers; ++l) {
@@ -493,7 +636,7 @@ static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* ou
         if (!last) { g.epi = EPI_ACT; g.act = m.act; }
         else if (last_epi == EPI_DESTD) { g.epi = EPI_DESTD; g.mean = mean; g.stdv = stdv; }
         else if (m.last_relu) { g.epi = EPI_ACT; g.act = KMPC_ACT_RELU; }
-        int rc = gemm(g, s);
+        int rc = gemm(g, s, part);
         if (rc) return rc;
         cur = dst;
         ldc = wmax;
@@ -530,6 +673,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     float* pong = (float*)p; p += align256(sizeof(float) * (size_t)Bn * wmax);
     float* z0 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
     float* z1 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
+    float* part = (float*)p;   // split-K partials (gemm(): only M N <= SPLITK_ELEMS outputs are split)
     int rc;
     dim3 tg((L + 31) / 32, (L + 31) / 32);
     hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
@@ -539,13 +683,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
 
     // ---- encode ----
     if (d->model_kind == KMPC_MODEL_GENERIC) {
-        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s, part);
         if (rc) return rc;
         if (d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, z0, Bn, L);
     } else {
         // c = We(x) (z1 holds c), z = shrink(c); loops: z = shrink(z S + c)   (model.py:200-209)
-        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z1, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s, part);
         if (rc) return rc;
         const size_t n = (size_t)Bn * L;
         hipLaunchKernelGGL(shrink_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z1, z0, n,
@@ -555,7 +699,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         for (int it = 0; it < d->lista_loops; ++it) {
             GemmArgs g = linear(Bn, L, L, zc, L, St, nullptr, zn, L);
             g.epi = EPI_SHRINK; g.R = z1; g.ldr = L; g.thr = d->lista_thresh; g.bf16 = bf;
-            if ((rc = gemm(g, s))) return rc;
+            if ((rc = gemm(g, s, part))) return rc;
             float* t = zc; zc = zn; zn = t;
         }
         if (zc != z0 && hipMemcpyAsync(z0, zc, sizeof(float) * n, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -569,6 +713,11 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
         la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
         la.ball = d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL;
+        if (Bn < 256 * LAT_ROWS) {   // 16 windows per block: twice the blocks of the 32-row kernel
+            const size_t lds = sizeof(float) * 2 * LAT16 * (L + 4);
+            hipLaunchKernelGGL(latent_steps16_kernel, dim3((Bn + LAT16 - 1) / LAT16), dim3(256), lds, s, la);
+            return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+        }
         const size_t lds = sizeof(float) * 2 * LAT_ROWS * (L + 4);
         hipLaunchKernelGGL(latent_steps_kernel, dim3((Bn + LAT_ROWS - 1) / LAT_ROWS), dim3(256), lds, s, la);
         return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
@@ -578,12 +727,12 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     for (int k = 0; k < H; ++k) {
         GemmArgs g = linear(Bn, L, L, zc, L, Kt, nullptr, zn, L);
         g.bf16 = bf;
-        if ((rc = gemm(g, s))) return rc;
+        if ((rc = gemm(g, s, part))) return rc;
         if (d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, zn, Bn, L);
         // decoder: hidden layers full width, last layer first-N rows + destandardize into yhat[:, k, :]
         rc = run_mlp(d->decoder, Bn, zn, L, yhat + (size_t)k * N, H * N, N, EPI_DESTD, d->mean, d->std,
-                     ping, pong, wmax, bf, s);
+                     ping, pong, wmax, bf, s, part);
         if (rc) return rc;
         float* t = zc; zc = zn; zn = t;
     }

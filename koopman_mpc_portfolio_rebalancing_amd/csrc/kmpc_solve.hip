@@ -44,10 +44,91 @@ __device__ __forceinline__ int wsumi(int v) {
     return v;
 }
 constexpr int SIMPLEX_WAVES = 4;   // windows per 256-thread block
+constexpr int SIMPLEX_HR = 16;     // register fast path: N <= 64 assets, H <= 16 periods
+
+// N <= 64, H <= 16 (BASELINE configs[1]: N = 30, H = 5): lane i holds R_t,i of its asset for every
+// period in registers (one pass over yhat, one np_expf per element), and each wave reduction runs
+// over all periods at once (H independent butterflies interleaved, instead of H dependent rounds).
+// Same arithmetic and order as the general loop below: bit-identical results.
+__device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane) {
+    constexpr int HR = SIMPLEX_HR;
+    const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
+    const float* y = a.yhat + (size_t)b * H * N;
+    const double* wp = a.wp + (size_t)b * N;
+    double* wout = a.wout + (size_t)b * tw * N;
+    const bool act = lane < N;
+    const double wpi = act ? wp[lane] : 0.0;
+    float R[HR];
+    int bad = !(isfinite(a.c) && isfinite(a.tau)) || (act && !isfinite(wpi));
+#pragma unroll
+    for (int t = 0; t < HR; ++t) {
+        R[t] = 0.0f;
+        if (t < H && act) {
+            R[t] = np_expf(y[(size_t)t * N + lane]);
+            bad |= !isfinite(R[t]);
+        }
+    }
+    if (wsumi(bad)) {
+        if (act)
+            for (int t = 0; t < tw; ++t) wout[(size_t)t * N + lane] = wpi;   // mpc.py:113-115
+        if (lane == 0) {
+            a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+            a.obj[b] = __builtin_nan("");
+            if (a.iters) a.iters[b] = 0;
+        }
+        return;
+    }
+    float rm[HR];
+    int cnt[HR];
+#pragma unroll
+    for (int t = 0; t < HR; ++t) rm[t] = R[t];
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int t = 0; t < HR; ++t)
+            if (t < H) rm[t] = fmaxf(rm[t], __shfl_xor(rm[t], o));
+#pragma unroll
+    for (int t = 0; t < HR; ++t) cnt[t] = (t < H && act && R[t] == rm[t]) ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int t = 0; t < HR; ++t)
+            if (t < H) cnt[t] += __shfl_xor(cnt[t], o);
+    double rw[HR], l1[HR];
+    double wprev = wpi;
+#pragma unroll
+    for (int t = 0; t < HR; ++t) {
+        rw[t] = l1[t] = 0.0;
+        if (t < H) {
+            const double w = 1.0 / cnt[t];
+            const double wi = (act && R[t] == rm[t]) ? w : 0.0;
+            rw[t] = (double)R[t] * wi;
+            l1[t] = act ? fabs(wi - wprev) : 0.0;
+            if (act && t < tw) wout[(size_t)t * N + lane] = wi;
+            wprev = wi;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int t = 0; t < HR; ++t)
+            if (t < H) { rw[t] += __shfl_xor(rw[t], o); l1[t] += __shfl_xor(l1[t], o); }
+    if (lane == 0) {
+        double f = 0.0;
+#pragma unroll
+        for (int t = 0; t < HR; ++t)
+            if (t < H) f += log(rw[t]) - a.c * l1[t];
+        a.status[b] = KMPC_STATUS_OPTIMAL;
+        a.obj[b] = f;
+        if (a.iters) a.iters[b] = 0;
+    }
+}
+
 __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a) {
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6);
     if (b >= a.B) return;   // (whole waves)
+    if (a.N <= 64 && a.H <= SIMPLEX_HR) {
+        simplex_regs(a, b, lane);
+        return;
+    }
     const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
     const float* y = a.yhat + (size_t)b * H * N;
     const double* wp = a.wp + (size_t)b * N;

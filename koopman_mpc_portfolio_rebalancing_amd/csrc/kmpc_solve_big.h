@@ -43,8 +43,14 @@ constexpr int NWX = 16;            // max waves per window (1024 threads)
 // slab stream is HBM-bound there: 768 slots measured -9% at N = 300, H = 15, equal at N = 500),
 // three (the LDS limit) for windows of <= 256 assets, which are latency-bound (N = 100, H = 20:
 // 512 -> 768 slots +17%, measured r02)
-constexpr int MAX_SLOTS = 512;
-constexpr int MAX_SLOTS_SMALL = 768;
+#ifndef KMPC_BIG_MAX_SLOTS
+#define KMPC_BIG_MAX_SLOTS 512
+#endif
+#ifndef KMPC_BIG_MAX_SLOTS_SMALL
+#define KMPC_BIG_MAX_SLOTS_SMALL 768
+#endif
+constexpr int MAX_SLOTS = KMPC_BIG_MAX_SLOTS;
+constexpr int MAX_SLOTS_SMALL = KMPC_BIG_MAX_SLOTS_SMALL;
 __host__ __device__ inline int slots_for(int B, int N) {
     const int cap = N <= 256 ? MAX_SLOTS_SMALL : MAX_SLOTS;
     return B < cap ? B : cap;
@@ -257,13 +263,20 @@ struct Win {
         b = B;
         sbuf ^= 1;
     }
-    // corrector targets of (t, i) from the affine direction: rc + dx dl_aff - smu, written back
-    // (the dl_aff come from the predictor targets still in RC*; ipm_kernel's corrector rows)
+    // the predictor's complementarity targets rc = x l of (t, i), from the state (never stored:
+    // three arrays less to write and to read back in the predictor's sweeps)
+    __device__ __forceinline__ void xl(const St& e, double& r1, double& r2, double& r3) const {
+        r1 = hw() ? e.w * e.l1 : 0.0;
+        r2 = hs() ? (e.s - e.d) * e.l2 : 0.0;
+        r3 = hs() ? (e.s + e.d) * e.l3 : 0.0;
+    }
+    // corrector targets of (t, i) from the affine direction: x l + dx dl_aff - smu, written to RC*
+    // (ipm_kernel's corrector rows)
     __device__ __forceinline__ void corr_rc(int t, const St& e, const Pre& p, double dd, double smu,
                                             double& r1, double& r2, double& r3) const {
         const double dw = p.dw, ds = p.ds;
-        const double rc1 = hw() ? p.rc1 : 0.0;
-        const double rc2 = hs() ? p.rc2 : 0.0, rc3 = hs() ? p.rc3 : 0.0;
+        double rc1, rc2, rc3;
+        xl(e, rc1, rc2, rc3);
         double dl1, dl2, dl3;
         ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
         r1 = rc1;
@@ -332,6 +345,8 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
     bool ok = true;
     St cur{};
     double W1c = 0.0, Ec = 0.0, pi = 0.0, lr = 0.0;
+    double pm = 1.0;   // prod_{1<=k<=t} max(Lr_k, LR_FLOOR) = pm 2^pe (renormalised: no underflow)
+    int pe = 0;
     if (W.act) {
         cur = W.st(0, W.wpi);
         W1c = cur.l1 * cur.iw;
@@ -360,15 +375,17 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             W.at(A_P, t) = cur.P;
             W.at(A_BP, t) = cur.bma * cur.P;
             W.at(A_BMA, t) = cur.bma;
-            W.at(A_RC1, t) = r1;
-            W.at(A_RC2, t) = r2;
-            W.at(A_RC3, t) = r3;
             // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
             const double Dd = pi + (nx ? En : 0.0);
             ok = ok && (Dd > 0.0) && (Dd < 1e300);
             const double iDd = rcp(Dd);
             W.at(A_IDD, t) = iDd;
             W.at(A_LR, t) = lr;
+            if (t) {
+                int ex;
+                pm = frexp(pm * fmax(lr, LR_FLOOR), &ex);
+                pe += ex;
+            }
             if (nx) {
                 lr = En * iDd;
                 pi = W1n + lr * pi;
@@ -376,6 +393,14 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             cur = nxt;
         }
         W.slot(t, P);
+    }
+    if (W.act) {
+        // the Schur generators' centred pi_{H-1} (ph_gram runs its pi recursion backward from it):
+        // pi_{H-1} = m 2^e, m in [0.5, 1) -> pi_{H-1} 2^-(e/2); X is free until the Newton solves
+        int e2;
+        const double m = frexp(pm, &e2);
+        const int e = pe + e2;
+        W.at(A_X, 0) = ldexp(m, e - e / 2);
     }
     W.finish(H);
     if (threadIdx.x < HM) {
@@ -418,44 +443,47 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
     auto& sh = W.sh;
     const int H = W.H, K3 = 3 * H, N4 = (W.N + 3) & ~3;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    // diagonal of Q^{-1} (dq_t = 1/Dd_t + Lr_{t+1}^2 dq_{t+1}) into X; pi_H for the centring
-    int e = 0;
-    if (W.act) {
-        double dqn = 0.0, lrn = 0.0, pi = 1.0;
+    // One backward sweep: dq_t = 1/Dd_t + Lr_{t+1}^2 dq_{t+1} (diagonal of Q^{-1}), the centred
+    // pi_t = pi_{t+1} / max(Lr_{t+1}, floor) from ph_factor's pi_{H-1} (X[0]), g = 1 / pi,
+    // beta = dq pi. The v-type generators need period t-1's g / beta: period t's are written at
+    // step t-1 (and period 0's after the loop), as is the direct (v_t, v_t) sum.
+    {
+        double pi = W.act ? (double)W.at(A_X, 0) : 1.0;
+        double dqn = 0.0, lrn = 0.0, gn = 0.0, bn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
-            const double dq = W.at(A_IDD, t) + lrn * lrn * dqn;
-            W.at(A_X, t) = dq;
-            dqn = dq;
-            lrn = W.at(A_LR, t);
-            if (t) pi *= fmax(lrn, LR_FLOOR);
+            double vvn = 0.0;
+            if (W.act) {
+                const double idd = W.at(A_IDD, t), lr = W.at(A_LR, t);
+                const double dq = idd + lrn * lrn * dqn;
+                if (t + 1 < H) pi *= rcp(fmax(lrn, LR_FLOOR));
+                const double al = W.alpha(t, W.at(A_M, t)), ep = W.epsa(t);
+                const double gt = rcp(pi), bt = dq * pi;
+                W.lg(3 * t + 1)[W.i] = al * gt;
+                W.lg(3 * t + 2)[W.i] = gt;
+                W.rg(3 * t + 1)[W.i] = al * bt;
+                W.rg(3 * t + 2)[W.i] = bt;
+                if (t + 1 < H) {
+                    W.lg(3 * t + 3)[W.i] = epn * (gn - gt);
+                    W.rg(3 * t + 3)[W.i] = epn * (bn - bt);
+                    // (v_{t+1}, v_{t+1}) = eps^2 (Qi[t+1][t+1] - 2 Qi[t][t+1] + Qi[t][t]), Qi[t][t+1] = Lr_{t+1} dq_{t+1}
+                    vvn = epn * epn * (dqn - 2.0 * lrn * dqn + dq);
+                }
+                if (t == 0) {
+                    W.lg(0)[W.i] = ep * gt;
+                    W.rg(0)[W.i] = ep * bt;
+                }
+                dqn = dq;
+                lrn = lr;
+                gn = gt;
+                bn = bt;
+                epn = ep;
+            } else if (W.i < N4) {
+                // padding assets of the last K group of the MFMA loop contribute zeros
+                for (int ty = 0; ty < 3; ++ty) { W.lg(3 * t + ty)[W.i] = 0.0; W.rg(3 * t + ty)[W.i] = 0.0; }
+            }
+            if (t + 1 < H) W.slot(t + 1, vvn);
         }
-        frexp(pi, &e);
-    }
-    const double cen = ldexp(1.0, -(e / 2));
-    double pi = 1.0, gp = 0.0, bp = 0.0, dqp = 0.0;
-    for (int t = 0; t < H; ++t) {
-        double vv = 0.0;
-        if (W.act) {
-            const double lr = W.at(A_LR, t), dq = W.at(A_X, t);
-            if (t) pi *= fmax(lr, LR_FLOOR);
-            const double al = W.alpha(t, W.at(A_M, t)), ep = W.epsa(t);
-            const double pt = pi * cen, gt = 1.0 / pt, bt = dq * pt;
-            W.lg(3 * t)[W.i] = ep * (gt - gp);
-            W.lg(3 * t + 1)[W.i] = al * gt;
-            W.lg(3 * t + 2)[W.i] = gt;
-            W.rg(3 * t)[W.i] = ep * (bt - bp);
-            W.rg(3 * t + 1)[W.i] = al * bt;
-            W.rg(3 * t + 2)[W.i] = bt;
-            // (v_t, v_t) = ep^2 (Qi[t][t] - 2 Qi[t-1][t] + Qi[t-1][t-1]), Qi[t-1][t] = Lr_t dq_t
-            vv = t ? ep * ep * (dq - 2.0 * lr * dq + dqp) : ep * ep * dq;
-            gp = gt;
-            bp = bt;
-            dqp = dq;
-        } else if (W.i < N4) {
-            // padding assets of the last K group of the MFMA loop contribute zeros
-            for (int ty = 0; ty < 3; ++ty) { W.lg(3 * t + ty)[W.i] = 0.0; W.rg(3 * t + ty)[W.i] = 0.0; }
-        }
-        W.slot(t, vv);
+        W.slot(0, W.act ? epn * epn * dqn : 0.0);   // (v_0, v_0) = eps_0^2 dq_0
     }
     W.finish(H);   // (its barriers also publish the generators to the workgroup)
     if ((int)threadIdx.x < H) sh.G[(3 * threadIdx.x) * LDG + 3 * threadIdx.x] = sh.tot[threadIdx.x];
@@ -574,15 +602,13 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         St cur{};
         double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0, r0c = 0.0, r1c = 0.0;
         if (W.act) {
-            const auto p = W.pre(0, corr, first, !first);
+            const auto p = W.pre(0, corr, false, !first);
             cur = W.st(p, W.wpi);
             if (corr) {
                 dwc = p.dw;
                 W.corr_rc(0, cur, p, dwc, smu, rc1c, rc2c, rc3c);
             } else if (first) {
-                rc1c = hw ? p.rc1 : 0.0;
-                rc2c = hs ? p.rc2 : 0.0;
-                rc3c = hs ? p.rc3 : 0.0;
+                W.xl(cur, rc1c, rc2c, rc3c);
             }
             r0c = p.r0;
             r1c = p.r1;
@@ -594,15 +620,13 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 St nxt = cur;
                 double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0, r0n = 0.0, r1n = 0.0;
                 if (nx) {
-                    const auto p = W.pre(t + 1, corr, first, !first);
+                    const auto p = W.pre(t + 1, corr, false, !first);
                     nxt = W.st(p, cur.w);
                     if (corr) {
                         dwn = p.dw;
                         W.corr_rc(t + 1, nxt, p, dwn - dwc, smu, rc1n, rc2n, rc3n);
                     } else if (first) {
-                        rc1n = hw ? p.rc1 : 0.0;
-                        rc2n = hs ? p.rc2 : 0.0;
-                        rc3n = hs ? p.rc3 : 0.0;
+                        W.xl(nxt, rc1n, rc2n, rc3n);
                     }
                     r0n = p.r0;
                     r1n = p.r1;
@@ -843,26 +867,29 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
 // c1, c2 of the asset complementarity along it, sum (x + a dx)(l + a dl) = c0 + a c1 + a^2 c2
 // (c0: ph_factor's mu sum) — the Mehrotra centring then needs no sweep of its own (ipm_kernel
 // max_step does the same).
+// pred: the predictor's direction, whose targets are x l (from the state, not stored)
 template <int HM, int FL>
-__device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2) {
+__device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2, bool pred) {
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
     double a = 1e300, wprev = W.wpi, dwp = 0.0;
     c1 = c2 = 0.0;
     typename Win<HM, FL>::Pre pn{};
-    if (W.act) pn = W.pre(0);
+    if (W.act) pn = W.pre(0, true, !pred);
     for (int t = 0; t < H; ++t) {
         double mdw = 0.0;
         if (W.act) {
             const auto p = pn;
-            if (t + 1 < H) pn = W.pre(t + 1);
+            if (t + 1 < H) pn = W.pre(t + 1, true, !pred);
             const St e = W.st(p, wprev);
             wprev = e.w;
             const double dw = p.dw, ds = p.ds, dd = dw - dwp;
             dwp = dw;
+            double r1 = p.rc1, r2 = p.rc2, r3 = p.rc3;
+            if (pred) W.xl(e, r1, r2, r3);
             double dl1, dl2, dl3;
-            W.ddirs(e, p.rc1, p.rc2, p.rc3, dw, ds, dd, dl1, dl2, dl3);
+            W.ddirs(e, r1, r2, r3, dw, ds, dd, dl1, dl2, dl3);
             if (hw) {
                 a = to_bound(e.w, dw, a); a = to_bound(e.l1, dl1, a);
                 c1 += e.w * dl1 + e.l1 * dw;
@@ -981,7 +1008,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         for (int pass = 0; pass < 2; ++pass) {
             ph_newton(W, (pass == 0 || mu > (W.hw() ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : a.n_refine, pass == 1, smu);
             double cc1, cc2;
-            const double amax = ph_step(W, cc1, cc2);
+            const double amax = ph_step(W, cc1, cc2, pass == 0);
             if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
             const double ap = fmin(1.0, amax);
             double comp = mu_l + ap * (cc1 + ap * cc2);

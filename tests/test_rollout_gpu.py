@@ -204,10 +204,12 @@ def test_bf16_lista_rollout_at_config5_shape():
 
 @pytest.mark.parametrize("norm,L,N,B,H", [("id", 64, 20, 1000, 4), ("ball", 64, 40, 333, 3),
                                           ("id", 128, 30, 4096, 5), ("ball", 256, 100, 70, 10),
-                                          ("id", 512, 50, 300, 6)])   # L = 512: 132 KB of LDS
+                                          ("id", 512, 50, 300, 6),     # L = 512: 132 KB of LDS
+                                          ("ball", 64, 20, 8200, 3)])  # >= 8192 windows: 32-row blocks
 def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
-    """The one-launch H-step loop (latent_steps_kernel: L % 32 == 0, single-layer decoder) against
-    the per-step GEMM launches (debug switch) and the numpy restatement."""
+    """The one-launch H-step loop (latent_steps_kernel: L % 32 == 0, single-layer decoder; 16 windows
+    per block below 8,192 windows, 32 from there) against the per-step GEMM launches
+    (kmpc_rollout_desc.latent_unfused) and the numpy restatement."""
     import bench
     obs, hidden = N * 4, 64
     sd = bench.make_state_dict(obs, L, hidden, seed=3)
@@ -226,3 +228,31 @@ def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
     assert np.abs(yf - ref).max() <= 1e-4 * np.abs(ref).max()
     assert np.abs(yf - yu).max() <= 1e-5 * np.abs(yu).max()
+
+
+def test_small_batch_split_k_encoder_matches_numpy():
+    """BASELINE configs[1] shape (4,096 windows, obs 600, encoder [1024, 1024] -> latent 128, N = 30,
+    H = 5): the 128-wide last encoder layer has fewer 64 x 64 tiles than CUs and runs split-K (four
+    K slices summed in slice order by the epilogue kernel); the latent loop runs 16 windows per block.
+    Against the numpy fp32 restatement and the per-step (unfused) launches."""
+    import bench
+    B, N, L, H, hidden = 4096, 30, 128, 5, 1024
+    obs = N * 20
+    sd = bench.make_state_dict(obs, L, hidden, seed=1)
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), torch.device("cuda"))
+    x = torch.randn(B, obs, generator=torch.Generator().manual_seed(2))
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    y = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
+    y2 = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
+    assert np.array_equal(y, y2)                        # deterministic split-K sum
+    sdn = {k: v.numpy() for k, v in sd.items()}
+    spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
+               "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],
+               "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None],
+               "norm_fn": bench.MODEL_CFG["MODEL"]["NORM_FN"]}
+    ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
+    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+    km.fuse_latent = False
+    yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
+    assert np.abs(y - yu).max() <= 1e-5 * np.abs(yu).max()

@@ -1,11 +1,10 @@
 #!/bin/bash
-# A/B of variant libraries on the C5 solve (tools/c5_probe.py): bash tools/ab_c5.sh libkmpc.so libkmpc_x.so
+# A/B of large-window variant libraries on the C5 solve (tools/c5_probe.py): bash tools/ab_c5.sh lib...
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/ab_c5.log
 for L in "$@"; do
   echo "== $L" >> gpurun_out/ab_c5.log
-  KMPC_DEV_LIB=$L REPS=2 timeout -k 10 120 python3 -u tools/c5_probe.py 1024 >> gpurun_out/ab_c5.log 2>&1 || exit $?
-  KMPC_DEV_LIB=$L REPS=2 PN=500 PH=10 timeout -k 10 120 python3 -u tools/c5_probe.py 2048 >> gpurun_out/ab_c5.log 2>&1 || exit $?
+  KMPC_DEV_LIB=$L REPS=3 timeout -k 10 120 python3 -u tools/c5_probe.py 1024 >> gpurun_out/ab_c5.log 2>&1 || exit $?
 done
 echo "exit 0"
