@@ -325,6 +325,45 @@ def secondary_c2(dev, steps: int, warmup: int) -> dict:
             "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
 
 
+def secondary_c1(dev, steps: int, warmup: int, B: int = 65536) -> dict:
+    """The BASELINE configs[0] model (10 assets, latent 128, H = 5, obs 200, encoder [1024, 1024],
+    MPCConfig(horizon=5, cost 1e-3, turnover cap 0.2) — the model and MPC of cpu_baseline_c1) with
+    its windows batched on the GPU: the small-window solve packs four windows per wave (16-lane
+    groups, kmpc_solve_kernel.h)."""
+    from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
+                                                       solve_mpc_log_utility_batched)
+    N, L, H, hidden = 10, 128, 5, 1024
+    obs = N * 20
+    model = DeviceKoopman(KoopmanModelSpec.from_state_dict(make_state_dict(obs, L, hidden, seed=10), MODEL_CFG), dev)
+    mean_d = torch.full((N,), 5e-4, dtype=torch.float32, device=dev)
+    std_d = torch.full((N,), 0.015, dtype=torch.float32, device=dev)
+    x, wp = window_inputs(0, B, N, obs, seed=10, device=dev)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, allow_short=False)
+    reps = max(steps, 1)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step():
+        y = model.rollout(x, mean_d, std_d, H, N)
+        return y, solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
+    for _ in range(max(warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        y, (W0, st, val, its) = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ev[0].record()
+    solve_mpc_log_utility_batched(wp, y, cfg)
+    ev[1].record()
+    torch.cuda.synchronize()
+    return {"workload": f"configs[0] model batched on the GPU: {B} windows, {N} assets, latent {L}, H={H}, obs {obs}, "
+                        f"enc [{hidden},{hidden}], c=1e-3 tau=0.2 no-short (packed solve: 4 windows per wave)",
+            "windows_per_s": B * reps / el, "ms_per_step": el / reps * 1e3, "steps": reps,
+            "solve_ms": ev[0].elapsed_time(ev[1]), "mean_ipm_iterations": float(its.float().mean().item()),
+            "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
+
+
 def make_lista_state_dict(obs: int, L: int, seed: int = 0) -> dict:
     """LISTAKM layout (model.py:190-209, 804-850) with LINEAR_ENCODER: the classic LISTA start
     We = D / Lc, S = I - D D^T / Lc for a random unit-row dictionary D [L, obs], Lc = 1.1 ||D||_2^2
@@ -497,6 +536,7 @@ def main():
         }
         if world == 1:
             line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
+            line["secondary_c1"] = secondary_c1(dev, args.steps, args.warmup)
             line["secondary_c5"] = secondary_c5(dev, min(args.steps, 3), min(args.warmup, 1))
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
