@@ -147,6 +147,17 @@ struct Win {
     __device__ __forceinline__ bool hs() const { return cs.hs; }
     __device__ __forceinline__ bool ht() const { return cs.ht; }
     __device__ __forceinline__ Ref at(int arr, int t) const { return Ref{rs, vo, (unsigned)((arr * HM + t) * NP) * 8u}; }
+    // m = R - 1 of (t, i): the slab keeps the float32 R (exact: (double)R - 1 is the kernels' m) in
+    // the first half of the M array's rows — half the bytes of the most-read input array
+    __device__ __forceinline__ double mload(int t) const {
+        const unsigned so = (unsigned)(A_M * HM * NP) * 8u + (unsigned)(t * NP) * 4u;
+        return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo >> 1, so, 0)) - 1.0;
+    }
+    __device__ __forceinline__ void mstore(int t, float r) const {
+        const unsigned so = (unsigned)(A_M * HM * NP) * 8u + (unsigned)(t * NP) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b32(rs, 0u, 0u, 0)), r),
+                                              rs, vo >> 1, so, 0);
+    }
     __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
     __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
     __device__ __forceinline__ double wprev(int t) const { return t ? at(A_W, t - 1) : wpi; }
@@ -165,7 +176,7 @@ struct Win {
         p.l1 = at(A_L1, t);
         p.l2 = at(A_L2, t);
         p.l3 = at(A_L3, t);
-        p.m = at(A_M, t);
+        p.m = mload(t);
         if (dir) { p.dw = at(A_DW, t); p.ds = at(A_DS, t); }
         if (rc) { p.rc1 = at(A_RC1, t); p.rc2 = at(A_RC2, t); p.rc3 = at(A_RC3, t); }
         if (rr) { p.r0 = at(A_R0, t); p.r1 = at(A_R1, t); }
@@ -188,7 +199,7 @@ struct Win {
         e.l1 = at(A_L1, t);
         e.l2 = at(A_L2, t);
         e.l3 = at(A_L3, t);
-        e.m = at(A_M, t);
+        e.m = mload(t);
         return derive(e, wp);
     }
     __device__ __forceinline__ St derive(St e, double wp) const {
@@ -322,7 +333,7 @@ __device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
         double mw = 0.0, w = 0.0, s = 0.0;
         if (W.act) {
             w = W.at(A_W, t);
-            mw = W.at(A_M, t) * w;
+            mw = W.mload(t) * w;
             s = W.at(A_S, t);
         }
         W.slot(3 * t, mw);
@@ -456,7 +467,7 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
                 const double idd = W.at(A_IDD, t), lr = W.at(A_LR, t);
                 const double dq = idd + lrn * lrn * dqn;
                 if (t + 1 < H) pi *= rcp(fmax(lrn, LR_FLOOR));
-                const double al = W.alpha(t, W.at(A_M, t)), ep = W.epsa(t);
+                const double al = W.alpha(t, W.mload(t)), ep = W.epsa(t);
                 const double gt = rcp(pi), bt = dq * pi;
                 W.lg(3 * t + 1)[W.i] = al * gt;
                 W.lg(3 * t + 2)[W.i] = gt;
@@ -693,7 +704,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 x = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * xn;
                 W.at(A_X, t) = x;
                 ep = W.epsa(t);
-                va = W.alpha(t, W.at(A_M, t)) * x;
+                va = W.alpha(t, W.mload(t)) * x;
                 vv1 = (t + 1 < H) ? epn * (xn - x) : 0.0;
                 lrn = W.at(A_LR, t);
             }
@@ -715,7 +726,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             double epc = W.epsa(0);
             for (int t = 0; t < H; ++t) {
                 const double epn = (t + 1 < H) ? W.epsa(t + 1) : 0.0;
-                const double zq = W.alpha(t, W.at(A_M, t)) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
+                const double zq = W.alpha(t, W.mload(t)) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
                                   ((t + 1 < H) ? epn * sh.q[3 * t + 3] : 0.0);
                 y = zq + W.at(A_LR, t) * y;
                 W.at(A_Y, t) = y;
@@ -800,7 +811,7 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
             double va = 0.0, vs = 0.0, vw = 0.0;
             if (W.act) {
                 vw = W.at(A_DW, t);
-                va = W.alpha(t, W.at(A_M, t)) * vw;
+                va = W.alpha(t, W.mload(t)) * vw;
                 vs = W.at(A_DS, t);
             }
             W.slot(t, va);
@@ -1050,9 +1061,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         if (W.act) {
             if (!isfinite(W.wpi)) nf = 1.0;
             for (int t = 0; t < H; ++t) {
-                const double m = np_expm1_d(yh[t * N + i]);
+                const float r = np_expf(yh[t * N + i]);
+                const double m = (double)r - 1.0;
                 if (!isfinite(m)) nf = 1.0;
-                W.at(A_M, t) = m;
+                W.mstore(t, r);
                 mx = fmax(mx, fabs(m));
             }
         }
@@ -1075,17 +1087,17 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         if (nf == 0.0 && isfinite(a.c) && isfinite(a.tau)) {
             if (a.allow_short && !hs) {
                 // no bounds and no turnover terms: unbounded unless every period is flat
-                for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.at(A_M, t) : 0.0);
+                for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.mload(t) : 0.0);
                 W.finish(H);
                 double spread = 0.0, swp = W.wpi;
                 if (W.act)
-                    for (int t = 0; t < H; ++t) spread = fmax(spread, fabs(W.at(A_M, t) - sh.tot[t] / N));
+                    for (int t = 0; t < H; ++t) spread = fmax(spread, fabs(W.mload(t) - sh.tot[t] / N));
                 W.sum_max(swp, spread);
                 if (spread == 0.0) {
                     const double w = swp != 0.0 ? W.wpi / swp : 1.0 / N;
                     for (int t = 0; t < H; ++t) {
                         if (W.act && t < tw) wout[t * N + i] = w;
-                        W.slot(t, W.act ? (1.0 + W.at(A_M, t)) * w : 0.0);
+                        W.slot(t, W.act ? (1.0 + W.mload(t)) * w : 0.0);
                     }
                     W.finish(H);
                     double f = 0.0;
