@@ -12,11 +12,14 @@ import sqlite3
 import sys
 
 
+KERNEL = "%ipm_kernel<10, 128, true, 7%"   # the C3 launch (the bench also runs other ipm_kernel instances)
+
+
 def mean(db, counter):
     con = sqlite3.connect(db)
     try:
-        r = con.execute("select avg(value) from counters_collection where kernel_name like '%ipm_kernel%' "
-                        "and counter_name = ?", (counter,)).fetchone()
+        r = con.execute("select avg(value) from counters_collection where kernel_name like ? "
+                        "and counter_name = ?", (KERNEL, counter)).fetchone()
     finally:
         con.close()
     return float(r[0]) if r and r[0] is not None else None
@@ -25,8 +28,8 @@ def mean(db, counter):
 def kernel_name(db):
     con = sqlite3.connect(db)
     try:
-        r = con.execute("select kernel_name from counters_collection where kernel_name like '%ipm_kernel%' "
-                        "limit 1").fetchone()
+        r = con.execute("select kernel_name from counters_collection where kernel_name like ? limit 1",
+                        (KERNEL,)).fetchone()
     finally:
         con.close()
     return r[0] if r else None
