@@ -5,6 +5,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import bench
 from koopman_mpc_portfolio_rebalancing_amd import DeviceKoopman, KoopmanModelSpec, MPCConfig, solve_mpc_log_utility_batched
+from koopman_mpc_portfolio_rebalancing_amd import _lib
+if os.environ.get("KMPC_DEV_LIB"):   # a variant library (csrc/Makefile tvar)
+    _lib._lib = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["KMPC_DEV_LIB"]))
 
 dev = torch.device("cuda", 0)
 B, N, L, H, hidden = int(os.environ.get("B", "4096")), 30, 128, 5, 1024
