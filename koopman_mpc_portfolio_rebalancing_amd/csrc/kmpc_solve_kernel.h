@@ -180,8 +180,8 @@ template <int D>
 __device__ __forceinline__ double dpp_partner(double v) {
     constexpr int ctrl = D == 8 ? 0x140 : (D == 4 ? 0x141 : (D == 2 ? 0x4e : 0xb1));
     const int2 x = as_i2(v);
-    return as_f64(__builtin_amdgcn_update_dpp(0, x.x, ctrl, 0xf, 0xf, false),
-                  __builtin_amdgcn_update_dpp(0, x.y, ctrl, 0xf, 0xf, false));
+    return as_f64(__builtin_amdgcn_mov_dpp(x.x, ctrl, 0xf, 0xf, false),
+                  __builtin_amdgcn_mov_dpp(x.y, ctrl, 0xf, 0xf, false));
 }
 template <int D>
 __device__ __forceinline__ double partner(double v) {   // value of the lane paired at level D
@@ -265,8 +265,8 @@ __device__ __forceinline__ double group_min(double v) {
 template <int C>
 __device__ __forceinline__ double dpp_f64(double v) {
     const int2 x = as_i2(v);
-    return as_f64(__builtin_amdgcn_update_dpp(0, x.x, C, 0xf, 0xf, false),
-                  __builtin_amdgcn_update_dpp(0, x.y, C, 0xf, 0xf, false));
+    return as_f64(__builtin_amdgcn_mov_dpp(x.x, C, 0xf, 0xf, false),
+                  __builtin_amdgcn_mov_dpp(x.y, C, 0xf, 0xf, false));
 }
 // lane j of every 16-lane row to the whole row (DPP row_newbcast:j). j is a constant in every
 // (unrolled) caller, so the switch folds to one DPP move per dword.
@@ -305,6 +305,9 @@ __device__ __forceinline__ double gbcast(double v, int src) {
     }
 }
 
+#ifndef KMPC_RS_BANK   // bank-masked DPP moves for the row_mirror / row_half_mirror levels
+#define KMPC_RS_BANK 1
+#endif
 // one butterfly level of the reduce-scatter: pairs (v[j], v[j+h]), j < h
 template <int M, int D>
 __device__ __forceinline__ void rs_level(double (&v)[M], int& n, int& slot) {
@@ -318,6 +321,19 @@ __device__ __forceinline__ void rs_level(double (&v)[M], int& n, int& slot) {
                     double a = v[j], b = v[j + h];
                     if constexpr (D == 32) swap32(a, b); else swap16(a, b);
                     v[j] = a + b;   // lower lanes: slot j, upper lanes: slot j + h
+                } else if constexpr (KMPC_RS_BANK && (D == 8 || D == 4)) {
+                    // the mirror permutations pair whole DPP banks (4 lanes): lower lanes are banks
+                    // {0, 1} (D = 8) / {0, 2} (D = 4) of each row. Two bank-masked moves per dword
+                    // instead of the lane selects: lower lanes take the partner's lo next to their
+                    // own lo, upper lanes the partner's hi next to their own hi.
+                    constexpr int ctrl = D == 8 ? 0x140 : 0x141;
+                    constexpr int lowm = D == 8 ? 0x3 : 0x5, upm = D == 8 ? 0xc : 0xa;
+                    const int2 lo = as_i2(v[j]), hi = as_i2(v[j + h]);
+                    const double t = as_f64(__builtin_amdgcn_update_dpp(hi.x, lo.x, ctrl, 0xf, lowm, false),
+                                            __builtin_amdgcn_update_dpp(hi.y, lo.y, ctrl, 0xf, lowm, false));
+                    const double u = as_f64(__builtin_amdgcn_update_dpp(lo.x, hi.x, ctrl, 0xf, upm, false),
+                                            __builtin_amdgcn_update_dpp(lo.y, hi.y, ctrl, 0xf, upm, false));
+                    v[j] = t + u;
                 } else {
                     const double lo = v[j], hi = v[j + h];
                     const double send = up ? lo : hi;
@@ -444,6 +460,11 @@ struct Thread : Case<FL> {
     static constexpr int GLN = GL;   // lanes per window (lane groups)
     static constexpr bool L = cold_in_lds<HM, MAXT, CS, QL, GL, FL>();
     int H, N, i;
+    // act: this lane's asset exists (i < N). Inactive lanes keep a zero iterate (w = s = l = m = 0,
+    // w_prev = 0) and neutral factors (zero slack reciprocals and P, unit pivots, zero dq), so what
+    // they add to any block sum is exactly zero and their direction stays zero; act is tested only
+    // where that does not follow (the factor, the Newton right-hand side and direction, residual
+    // norms, memory writes) — not in every per-period body.
     bool act;
     double c, tau, sig, isig, irsig, wpi;
     // state
@@ -890,7 +911,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         tq[t] = 0.0;
-        if (T.act && t < H) {
+        if (t < H) {   // (inactive lanes: masked in the dw line below)
             const double al = T.m[t] * sh.iden[t] * T.irsig;
             double v = al * sh.bs[t] + sh.bs[2 * HM + t];
             if (T.ht) {
@@ -912,7 +933,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
         }
         R.periods(px);
 #pragma unroll
-        for (int t = 0; t < HM; ++t) bs[t] = (T.act && t < H) ? T.P[t] * (bs[t] - sh.rho[t] * px[t]) : 0.0;
+        for (int t = 0; t < HM; ++t) bs[t] = t < H ? T.P[t] * (bs[t] - sh.rho[t] * px[t]) : 0.0;   // (P = 0: inactive)
     } else {
 #pragma unroll
         for (int t = 0; t < HM; ++t) bs[t] = 0.0;
@@ -948,7 +969,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         r0[t] = r1[t] = 0.0;
-        if (T.act && t < H) {
+        if (t < H) {   // (inactive lanes' rows are masked in lsolve; their norm below)
             double rdw, rds;
             dual_residual<HM, NWM>(T, sh, t, rdw, rds);
             r0[t] = -rdw;
@@ -957,8 +978,11 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
                 bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)),
                                    fmax(fabs(T.rc1[t]), fmax(fabs(T.rc2[t]), fabs(T.rc3[t])))));
         }
-        if (gvt<TH::GLN>() == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     }
+    if (!T.act) bn = 0.0;
+#pragma unroll
+    for (int t = 0; t < HM; ++t)
+        if (gvt<TH::GLN>() == 0 && t < H) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     if (n_refine > 0) bn = R.max1(bn);
     KMPC_PH(np, 12);
     int r = 0;
@@ -985,7 +1009,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         double adw[HM], sds[HM], sdw[HM];
 #pragma unroll
         for (int t = 0; t < HM; ++t) {
-            const bool on = T.act && t < H;
+            const bool on = t < H;   // (inactive lanes: dw = ds = 0)
             adw[t] = on ? T.m[t] * sh.iden[t] * T.irsig * T.dw[t] : 0.0;
             sds[t] = on ? T.ds[t] : 0.0;
             sdw[t] = on ? T.dw[t] : 0.0;
@@ -997,7 +1021,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         for (int t = HM - 1; t >= 0; --t) {
             double dl1, dl2, dl3;
             T.dual_dirs(t, dl1, dl2, dl3);
-            if (T.act && t < H) {
+            if (t < H) {   // (inactive lanes' rows: masked in lsolve and in rn below)
                 double rdw, rds;
                 dual_residual<HM, NWM>(T, sh, t, rdw, rds);
                 const double al = T.m[t] * sh.iden[t] * T.irsig;
@@ -1012,6 +1036,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
             nl2 = (t < H) ? dl2 : 0.0;
             nl3 = (t < H) ? dl3 : 0.0;
         }
+        if (!T.act) rn = 0.0;   // (lane 0, the owner rows', is always active)
         rn = R.max1(rn);
         KMPC_PH(np, 14);
         if (rn <= REFINE_RTOL * bn) break;
@@ -1028,7 +1053,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     // dz4 / dl4 of the final direction
     double sds[HM];
 #pragma unroll
-    for (int t = 0; t < HM; ++t) sds[t] = (T.act && t < H) ? T.ds[t] : 0.0;
+    for (int t = 0; t < HM; ++t) sds[t] = t < H ? T.ds[t] : 0.0;   // (inactive lanes: ds = 0)
     const double st_own = R.own1(sds);
     if (gvt<TH::GLN>() < HM) {
         const int t = gvt<TH::GLN>();
@@ -1059,7 +1084,7 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         mdw[t] = 0.0;
-        if (T.act && t < H) {
+        if (t < H) {   // (inactive lanes: zero iterate, direction and reciprocals -> no bound, zero sums)
             const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
             const double d = T.w[t] - T.wprev(t);
             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
@@ -1179,8 +1204,9 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     __syncthreads();   // sh.rho / sh.sr / sh.flag visible
     if (!ok) sh.flag = 1;
     // column coefficients of this asset: alpha_t (a), eps_t (v)
-    auto al = [&](int t) -> double { return (T.act && t < H) ? T.m[t] * sh.iden[t] * T.irsig : 0.0; };
-    auto ep = [&](int t) -> double { return (T.act && t < H && T.ht) ? sh.sr[t] * T.bma(t) * T.P[t] : 0.0; };
+    // (inactive lanes: m = 0 and P = 0, so both coefficients vanish, as does dq)
+    auto al = [&](int t) -> double { return t < H ? T.m[t] * sh.iden[t] * T.irsig : 0.0; };
+    auto ep = [&](int t) -> double { return (t < H && T.ht) ? sh.sr[t] * T.bma(t) * T.P[t] : 0.0; };
     const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
     if constexpr (static_gram<HM, NWM>()) {
         // Static-slot Gram: every entry (j, l) of G with period(j) <= period(l) = c has a
@@ -1434,7 +1460,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
     auto& sh = shv[grp<GL>()];
     const int b = blockIdx.x * WPB + grp<GL>();
     if (b >= args.B) return;   // (whole groups of the last block)
-    const int nw = GL == 64 ? (int)(blockDim.x / WAVE) : 1;
+    // waves in the block: a compile-time constant up to 128 threads (the launchers use MAXT = 128
+    // only for 128-thread blocks), so the reductions' per-wave slot loops need no run-time guards
+    const int nw = GL < 64 ? 1 : (MAXT <= 128 ? NWM : (int)(blockDim.x / WAVE));
     Reducer<HM, NWM, GL> R(sh, nw);
     Thread<HM, MAXT, FL, CS, QL, GL> T;
     T.bind_cold();
@@ -1539,7 +1567,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     double mw[HM], sw[HM], ssum[HM], l1n[HM];
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
-                        const bool on = T.act && t < H;
+                        const bool on = t < H;   // (inactive lanes: zero iterate)
                         mw[t] = on ? T.m[t] * T.w[t] : 0.0;
                         sw[t] = on ? T.w[t] : 0.0;
                         ssum[t] = on ? T.s[t] : 0.0;
@@ -1569,7 +1597,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 double mu_l = 0.0, rd = 0.0;
 #pragma unroll
                 for (int t = 0; t < HM; ++t) {
-                    if (T.act && t < H) {
+                    if (t < H) {
                         const double d = T.w[t] - T.wprev(t);
                         double rdw, rds;
                         dual_residual<HM, NWM>(T, sh, t, rdw, rds);
@@ -1578,6 +1606,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                         rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
                     }
                 }
+                if (!T.act) rd = 0.0;   // (an inactive lane's mu terms are zero; its dual rows are not rows)
                 double mu;
                 R.sum_max(mu_l, rd, mu, rd);
                 const double mu_assets = mu;   // c0 of the complementarity polynomial (max_step)
@@ -1617,7 +1646,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
 #pragma unroll
                 for (int t = 0; t < HM; ++t) {
                     double r1 = 0.0, r2 = 0.0, r3 = 0.0;
-                    if (T.act && t < H) {
+                    if (t < H) {   // (inactive lanes: zero)
                         const double d = T.w[t] - T.wprev(t);
                         r1 = T.hw ? T.w[t] * T.l1[t] : 0.0;
                         r2 = T.hs ? (T.s[t] - d) * T.l2[t] : 0.0;
@@ -1663,7 +1692,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
-                        if (T.act && t < H) {
+                        if (t < H) {   // (inactive lanes: -smu, multiplied by zero reciprocals wherever read)
                             const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
                             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
                             if (T.hw) T.rc1.set(t, T.rc1[t] + (T.dw[t] * dl1 - smu));
@@ -1688,7 +1717,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
-                        if (T.act && t < H) {
+                        if (t < H) {   // (inactive lanes: zero direction)
                             T.l1[t] += step * DL1[t];
                             T.l2[t] += step * DL2[t];
                             T.l3[t] += step * DL3[t];
@@ -1697,7 +1726,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 }
 #pragma unroll
                 for (int t = 0; t < HM; ++t) {
-                    if (T.act && t < H) {
+                    if (t < H) {
                         T.w[t] += step * T.dw[t];
                         T.s[t] += step * T.ds[t];
                     }
