@@ -305,6 +305,12 @@ __device__ __forceinline__ double gbcast(double v, int src) {
     }
 }
 
+#ifndef KMPC_ZX_ONE   // Z^T x of the Newton solve as one reduce-scatter of the 3 H values
+#define KMPC_ZX_ONE 0
+#endif
+#ifndef KMPC_OPAQUE_LANE
+#define KMPC_OPAQUE_LANE 1
+#endif
 #ifndef KMPC_RS_BANK   // bank-masked DPP moves for the row_mirror / row_half_mirror levels
 #define KMPC_RS_BANK 1
 #endif
@@ -503,6 +509,14 @@ struct Thread : Case<FL> {
             x[t] = (t < H) ? v : 0.0;
             nxt = x[t];
         }
+    }
+
+    // the predictor's complementarity targets x l of period t, from the iterate
+    __device__ __forceinline__ void xl(int t, double& r1, double& r2, double& r3) const {
+        const double d = w[t] - wprev(t);
+        r1 = hw ? w[t] * l1[t] : 0.0;
+        r2 = hs ? (s[t] - d) * l2[t] : 0.0;
+        r3 = hs ? (s[t] + d) * l3[t] : 0.0;
     }
 
     // multipliers of the current direction for every period at once: the cold LDS reads of a
@@ -843,8 +857,32 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
     // x = Q^{-1} rhs_w (in bw) ;  bs = Z^T x  (block-summed over assets)
     T.qsolve(bw, bw);
     {
+#if KMPC_ZX_ONE
+        // the 3 H values (a, v, budget columns: slot k H + t) in one reduce-scatter of
+        // MP = pow2(3 H) slots, one barrier
+        constexpr int MP = pow2_at_least(3 * HM);
+        constexpr int MO = HM;   // slot offset of column type k
+        constexpr int RW = Shared<HM, NWM>::RW;
+        const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
+        double* rb = &sh.red[R.buf][0][0];
+        {
+            double v[MP];
+#pragma unroll
+            for (int q = 0; q < MP; ++q) {
+                const int k = q / HM, t = q - k * HM;
+                double val = 0.0;
+                if (k == 0) val = T.m[t] * sh.iden[t] * T.irsig * bw[t];
+                else if (k == 1) val = T.ht ? sh.sr[t] * T.bma(t) * T.P[t] * (bw[t] - (t ? bw[t - 1] : 0.0)) : 0.0;
+                else if (k == 2) val = bw[t];
+                v[q] = val;
+            }
+            const int slot = wave_reduce_scatter<MP, TH::GLN>(v);
+            if ((lane & ((TH::GLN / MP) - 1)) == 0) rb[wv * RW + slot] = v[0];
+        }
+#else
         // three chunks (a, v, budget columns) of MP = pow2(HM) slots, one barrier
         constexpr int MP = pow2_at_least(HM);
+        constexpr int MO = MP;
         constexpr int RW = Shared<HM, NWM>::RW;
         const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
         double* rb = &sh.red[R.buf][0][0];
@@ -864,6 +902,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
             const int slot = wave_reduce_scatter<MP, TH::GLN>(v);
             if ((lane & ((TH::GLN / MP) - 1)) == 0) rb[wv * RW + k * MP + slot] = v[0];
         }
+#endif
         __syncthreads();
         R.buf ^= Shared<HM, NWM>::NB - 1;
         KMPC_PH(lp, 9);
@@ -874,7 +913,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
                 const int k = lane / HM, t = lane % HM;
 #pragma unroll
                 for (int q = 0; q < NWM; ++q)
-                    if (q < R.nw) rhs += rb[q * RW + k * MP + t];
+                    if (q < R.nw) rhs += rb[q * RW + k * MO + t];
                 if (k == 2 && t < H) rhs -= sh.lb6[t];
             }
             // G = L D L^T with L unit lower, stored strictly lower (zero on and above the
@@ -958,7 +997,7 @@ __device__ __forceinline__ void newton_rows(const TH& T, Shared<HM, NWM>& sh, in
 // On exit: T.dw, T.ds, sh.dnu, sh.dz4, sh.dl4.
 template <int HM, int NWM, class TH>
 __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
-                                       int n_refine) {
+                                       int n_refine, bool pred) {
     const int H = T.H;
     PhaseClock np;
     KMPC_PH_START(np);
@@ -969,7 +1008,15 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #pragma unroll
     for (int t = 0; t < HM; ++t) {
         r0[t] = r1[t] = 0.0;
-        if (t < H) {   // (inactive lanes' rows are masked in lsolve; their norm below)
+        if (pred) {
+            // the predictor's (affine) right-hand side with its targets x l folded in: the dual rows
+            // minus the scaled complementarity rows x l / x = l cancel to m / (1 + m.w) / sig - nu
+            // (w rows) and -c - l4 (s rows), exactly — no target, reciprocal or multiplier read
+            if (t < H) {
+                r0[t] = T.m[t] * sh.iden[t] * T.isig - sh.nu[t];
+                r1[t] = T.hs ? -T.c - sh.l4[t] : 0.0;
+            }
+        } else if (t < H) {   // (inactive lanes' rows are masked in lsolve; their norm below)
             double rdw, rds;
             dual_residual<HM, NWM>(T, sh, t, rdw, rds);
             r0[t] = -rdw;
@@ -990,7 +1037,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #ifdef KMPC_STATS
         const unsigned long long t_ls = __builtin_amdgcn_s_memtime();
 #endif
-        lsolve<HM, NWM>(T, sh, R, r0, r1, r == 0);
+        lsolve<HM, NWM>(T, sh, R, r0, r1, r == 0 && !pred);
 #ifdef KMPC_STATS
         if (threadIdx.x == 0 && (blockIdx.x & 255) == 0) atomicAdd(&g_phase[7], __builtin_amdgcn_s_memtime() - t_ls);
 #endif
@@ -1214,7 +1261,10 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         // buf[s % 16]; a full chunk of 16 slots is reduce-scattered over the wave at once and the
         // wave totals go to sh.gred[wave][slot] (aliasing G, which is not live here).
         // static_for keeps every index a compile-time constant (no dynamic register indexing).
-        constexpr int CH = 16;
+#ifndef KMPC_GRAM_CH
+#define KMPC_GRAM_CH 32
+#endif
+        constexpr int CH = KMPC_GRAM_CH < TH::GLN ? KMPC_GRAM_CH : TH::GLN;
         constexpr int NS = gram_slots(HM);
         double ca[HM], ce[HM];
 #pragma unroll
@@ -1368,7 +1418,13 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     // (the column broadcast of the LDL^T steps uses reduction slots: no reduction is in flight here)
     double* col = &sh.red[0][0][0];
     if (gvt<TH::GLN>() < WAVE) {
-        const int r = lane;
+        int r = lane;
+#if KMPC_OPAQUE_LANE
+        // a fresh value per call: the lane comparisons of the unrolled steps (r > j, r == j) are
+        // then evaluated where used instead of being hoisted out of the IPM loop into ~60 SGPR
+        // pairs that spill to VGPR lanes (two v_readlane + hazard nops per use)
+        asm volatile("" : "+v"(r));
+#endif
         const bool rused = r < KM && (r % HM) < H && (r / HM != 1 || T.ht);
         double g[KM];
 #pragma unroll
@@ -1643,15 +1699,12 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                 if (mu < args.tol && rd < 10.0 * args.tol && pr < 10.0 * args.tol) break;
                 KMPC_PH(ph, 0);
                 if (!factor<HM, NWM>(T, sh, R, ph)) break;
+                // the predictor's targets rc = x l (read by its multipliers; its solve folds them into
+                // the right-hand side, newton())
 #pragma unroll
                 for (int t = 0; t < HM; ++t) {
                     double r1 = 0.0, r2 = 0.0, r3 = 0.0;
-                    if (t < H) {   // (inactive lanes: zero)
-                        const double d = T.w[t] - T.wprev(t);
-                        r1 = T.hw ? T.w[t] * T.l1[t] : 0.0;
-                        r2 = T.hs ? (T.s[t] - d) * T.l2[t] : 0.0;
-                        r3 = T.hs ? (T.s[t] + d) * T.l3[t] : 0.0;
-                    }
+                    if (t < H) T.xl(t, r1, r2, r3);   // (inactive lanes: zero)
                     T.rc1.set(t, r1);
                     T.rc2.set(t, r2);
                     T.rc3.set(t, r3);
@@ -1673,7 +1726,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { park[t] = T.w[t]; park[HM + t] = T.s[t]; }
                     asm volatile("" :: "v"(&park[0]) : "memory");
-                    newton<HM, NWM>(T, sh, R, (pass == 0 || mu > (T.hw ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : args.n_refine);
+                    newton<HM, NWM>(T, sh, R, (pass == 0 || mu > (T.hw ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : args.n_refine,
+                                    pass == 0);
                     asm volatile("" :: "v"(&park[0]) : "memory");
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { T.w[t] = park[t]; T.s[t] = park[HM + t]; }
@@ -1692,14 +1746,21 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     T.dual_dirs_all(DL1, DL2, DL3);
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
-                        if (t < H) {   // (inactive lanes: -smu, multiplied by zero reciprocals wherever read)
+                        // the corrector's targets x l + dx_aff dl_aff - sigma mu (inactive lanes:
+                        // -smu, multiplied by zero reciprocals wherever read)
+                        double r1 = 0.0, r2 = 0.0, r3 = 0.0;
+                        if (t < H) {
                             const double dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
                             const double dd = T.dw[t] - (t ? T.dw[t - 1] : 0.0);
-                            if (T.hw) T.rc1.set(t, T.rc1[t] + (T.dw[t] * dl1 - smu));
-                            if (T.hs) {
-                                T.rc2.set(t, T.rc2[t] + ((T.ds[t] - dd) * dl2 - smu));
-                                T.rc3.set(t, T.rc3[t] + ((T.ds[t] + dd) * dl3 - smu));
-                            }
+                            r1 = T.rc1[t]; r2 = T.rc2[t]; r3 = T.rc3[t];
+                            r1 += T.dw[t] * dl1 - smu;
+                            r2 += (T.ds[t] - dd) * dl2 - smu;
+                            r3 += (T.ds[t] + dd) * dl3 - smu;
+                        }
+                        if (T.hw) T.rc1.set(t, r1);
+                        if (T.hs) {
+                            T.rc2.set(t, r2);
+                            T.rc3.set(t, r3);
                         }
                     }
                     if (gvt<GL>() < HM && T.ht && (int)gvt<GL>() < H) {
