@@ -305,9 +305,6 @@ __device__ __forceinline__ double gbcast(double v, int src) {
     }
 }
 
-#ifndef KMPC_ZX_ONE   // Z^T x of the Newton solve as one reduce-scatter of the 3 H values
-#define KMPC_ZX_ONE 0
-#endif
 #ifndef KMPC_OPAQUE_LANE
 #define KMPC_OPAQUE_LANE 1
 #endif
@@ -857,7 +854,6 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
     // x = Q^{-1} rhs_w (in bw) ;  bs = Z^T x  (block-summed over assets)
     T.qsolve(bw, bw);
     {
-#if KMPC_ZX_ONE
         // the 3 H values (a, v, budget columns: slot k H + t) in one reduce-scatter of
         // MP = pow2(3 H) slots, one barrier
         constexpr int MP = pow2_at_least(3 * HM);
@@ -879,30 +875,6 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
             const int slot = wave_reduce_scatter<MP, TH::GLN>(v);
             if ((lane & ((TH::GLN / MP) - 1)) == 0) rb[wv * RW + slot] = v[0];
         }
-#else
-        // three chunks (a, v, budget columns) of MP = pow2(HM) slots, one barrier
-        constexpr int MP = pow2_at_least(HM);
-        constexpr int MO = MP;
-        constexpr int RW = Shared<HM, NWM>::RW;
-        const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
-        double* rb = &sh.red[R.buf][0][0];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            double v[MP];
-#pragma unroll
-            for (int t = 0; t < MP; ++t) {
-                double val = 0.0;
-                if (t < HM) {
-                    if (k == 0) val = T.m[t] * sh.iden[t] * T.irsig * bw[t];
-                    else if (k == 1) val = T.ht ? sh.sr[t] * T.bma(t) * T.P[t] * (bw[t] - (t ? bw[t - 1] : 0.0)) : 0.0;
-                    else val = bw[t];
-                }
-                v[t] = val;
-            }
-            const int slot = wave_reduce_scatter<MP, TH::GLN>(v);
-            if ((lane & ((TH::GLN / MP) - 1)) == 0) rb[wv * RW + k * MP + slot] = v[0];
-        }
-#endif
         __syncthreads();
         R.buf ^= Shared<HM, NWM>::NB - 1;
         KMPC_PH(lp, 9);
