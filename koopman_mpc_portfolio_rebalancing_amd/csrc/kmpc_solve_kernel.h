@@ -1132,12 +1132,12 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
         a = to_bound(sh.l4[t], sh.dl4[t], a);
     }
     a = R.periods_min_sums(mdw, a, c1, c2);
+    // the R.w > 0 bounds through the stored 1 / den: the largest -d(R.w) / (R.w), inverted once
+    double qr = 0.0;
 #pragma unroll
-    for (int t = 0; t < HM; ++t) {
-        if (t < H) {
-            a = to_bound(sh.den[t], mdw[t], a);
-        }
-    }
+    for (int t = 0; t < HM; ++t)
+        if (t < H) qr = fmax(qr, -mdw[t] * sh.iden[t]);
+    if (qr > 0.0) a = fmin(a, rcp_nr(qr));
     return a;
 }
 
