@@ -150,6 +150,35 @@ __device__ __forceinline__ void gram_slot_jl(int s, int& j, int& l) {
 
 
 
+// (j, l) of every static Gram slot, packed j | l << 8: one table load per slot where G is assembled
+// instead of gram_slot_jl's compare chain and divisions (KM <= 30 < 256)
+template <int HM>
+struct GramTab {
+    unsigned short v[gram_slots(HM)];
+    constexpr GramTab() : v() {
+        for (int s = 0; s < gram_slots(HM); ++s) {
+            int c = 0;
+            for (int k = 1; k < HM; ++k) c += (s >= 9 * k * (k - 1) / 2 + 6 * k) ? 1 : 0;
+            const int r = s - (9 * c * (c - 1) / 2 + 6 * c);
+            int tj, tyj, tyl;
+            if (r < 9 * c) {
+                tj = r / 9;
+                const int q = r - 9 * tj;
+                tyj = q / 3;
+                tyl = q - 3 * tyj;
+            } else {
+                tj = c;
+                const int q = r - 9 * c;
+                tyj = (q >= 3) + (q >= 5);
+                tyl = q < 3 ? q : (q < 5 ? q - 2 : 2);
+            }
+            v[s] = (unsigned short)((tyj * HM + tj) | ((tyl * HM + c) << 8));
+        }
+    }
+};
+template <int HM>
+__device__ constexpr GramTab<HM> kGramTab{};
+
 // ---- wave primitives ----------------------------------------------------------------------------
 // Cross-lane exchange without LDS: v_permlane32_swap / v_permlane16_swap (gfx950) for the two
 // upper butterfly levels and DPP mirror / quad permutations for the four lower ones. Every level
@@ -790,11 +819,11 @@ struct Reducer {
     }
 };
 
-// ratio test; the step is scaled by 0.99 afterwards, so the reciprocal (one Newton step on
-// v_rcp_f64) is exact enough and the test stays conservative to ~1e-15 relative
+// ratio test on the raw v_rcp_f64 estimate: the corrector's step is 0.99 of the bound, so a bound
+// off by its 2^-24 relative error still leaves every slack and multiplier >= 1% of its value (the
+// predictor's bound only sets sigma); a Newton step on the reciprocal cost 1.2% of the C3 solve
 __device__ __forceinline__ double to_bound(double v, double dv, double a) {
-    double r = __builtin_amdgcn_rcp(dv);
-    r = r * (2.0 - dv * r);
+    const double r = __builtin_amdgcn_rcp(dv);   // (2^-24 relative, measured: tools/dev/rcp_check)
     return (dv < 0.0) ? fmin(a, -v * r) : a;
 }
 
@@ -1288,7 +1317,9 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         });
         __syncthreads();
         // assemble both triangles of G: read the partials, barrier (gred aliases G), write
-        constexpr int SPT = (NS + TH::GLN - 1) / TH::GLN;
+        // slots per thread: blocks of <= 128 threads have exactly NWM waves; 256-thread blocks >= 3
+        constexpr int MINT = TH::GLN == 64 ? (NWM > 2 ? (NWM - 1) * 64 : NWM * 64) : TH::GLN;
+        constexpr int SPT = (NS + MINT - 1) / MINT;
         double tot[SPT];
 #pragma unroll
         for (int k = 0; k < SPT; ++k) {
@@ -1303,8 +1334,8 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
         for (int k = 0; k < SPT; ++k) {
             const int s = gvt<TH::GLN>() + k * (TH::GLN == 64 ? (int)blockDim.x : TH::GLN);
             if (s < NS) {
-                int j, l;
-                gram_slot_jl<HM>(s, j, l);
+                const int jl = kGramTab<HM>.v[s];
+                const int j = jl & 255, l = jl >> 8;
                 sh.G[j * KM + l] = tot[k];
                 sh.G[l * KM + j] = tot[k];
             }
