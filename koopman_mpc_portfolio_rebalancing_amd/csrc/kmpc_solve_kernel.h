@@ -775,6 +775,33 @@ struct Reducer {
         }
         buf ^= Shared<HM, NWM>::NB - 1;
     }
+    // block sum of s and block maxima of m1, m2, sharing one barrier
+    __device__ __forceinline__ void sum_max2(double s, double m1, double m2, double& S, double& M1, double& M2) {
+        constexpr int RW = Shared<HM, NWM>::RW;
+        const int lane = glane<GL>(), wv = gwave<GL>();
+        s = group_sum<GL>(s);
+        m1 = group_max<GL>(m1);
+        m2 = group_max<GL>(m2);
+        double* r = &sh.red[buf][0][0];
+        if (lane == 0) { r[wv * RW] = s; r[wv * RW + 1] = m1; r[wv * RW + 2] = m2; }
+        __syncthreads();
+        double ss[NWM], a1[NWM], a2[NWM];
+#pragma unroll
+        for (int q = 0; q < NWM; ++q) {
+            ss[q] = (q == 0 || q < nw) ? r[q * RW] : 0.0;
+            a1[q] = (q == 0 || q < nw) ? r[q * RW + 1] : 0.0;
+            a2[q] = (q == 0 || q < nw) ? r[q * RW + 2] : 0.0;
+        }
+        S = ss[0];
+        M1 = a1[0];
+        M2 = a2[0];
+#pragma unroll
+        for (int q = 1; q < NWM; ++q) {
+            S += ss[q];
+            if (q < nw) { M1 = fmax(M1, a1[q]); M2 = fmax(M2, a2[q]); }
+        }
+        buf ^= Shared<HM, NWM>::NB - 1;
+    }
     __device__ __forceinline__ double sum1(double x) {
         const int lane = glane<GL>(), wv = gwave<GL>();
         x = group_sum<GL>(x);
@@ -1159,6 +1186,9 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
         const int t = gvt<TH::GLN>();
         a = to_bound(sh.z4[t], sh.dz4[t], a);
         a = to_bound(sh.l4[t], sh.dl4[t], a);
+        // the cap's complementarity along the step, (z4 + a dz4)(l4 + a dl4) - z4 l4, in the same sums
+        c1 += sh.z4[t] * sh.dl4[t] + sh.l4[t] * sh.dz4[t];
+        c2 += sh.dz4[t] * sh.dl4[t];
     }
     a = R.periods_min_sums(mdw, a, c1, c2);
     // the R.w > 0 bounds through the stored 1 / den: the largest -d(R.w) / (R.w), inverted once
@@ -1621,6 +1651,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
             for (it = 0; it < args.max_iter; ++it) {
                 // ---- residuals: den_t = 1 + m.w, 1'w_t - 1, tau - 1's_t - z4 ----
                 double my_rw = 0.0;   // this period thread's R.w total
+                double own_rc4 = 0.0, own_pr = 0.0;   // this period thread's z4 l4, max(|rp|, |rg4|)
+                bool own_bad = false;                 // ... and R.w <= 0
                 double l1_own[HM];    // this asset's |w_t - w_{t-1}|, reduced only when the iterate is kept
                 {
                     double mw[HM], sw[HM], ssum[HM], l1n[HM];
@@ -1649,6 +1681,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                         sh.rg4[t] = (T.ht && on) ? T.tau - c2 - sh.z4[t] : 0.0;
                         sh.rc4[t] = (T.ht && on) ? sh.z4[t] * sh.l4[t] : 0.0;
                         sh.iz4[t] = 1.0 / sh.z4[t];
+                        if (on) {
+                            own_rc4 = sh.rc4[t];
+                            own_pr = fmax(fabs(sh.rp[t]), fabs(sh.rg4[t]));
+                            own_bad = !(sh.den[t] > 0.0);
+                        }
                         newton_rows<HM, NWM>(T, sh, t);   // the predictor's rows
                     }
                     __syncthreads();
@@ -1666,16 +1703,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     }
                 }
                 if (!T.act) rd = 0.0;   // (an inactive lane's mu terms are zero; its dual rows are not rows)
-                double mu;
-                R.sum_max(mu_l, rd, mu, rd);
-                const double mu_assets = mu;   // c0 of the complementarity polynomial (max_step)
-                double pr = 0.0;
-                bool domain_ok = true;
-                for (int t = 0; t < H; ++t) {
-                    mu += sh.rc4[t];
-                    pr = fmax(pr, fmax(fabs(sh.rp[t]), fabs(sh.rg4[t])));
-                    domain_ok = domain_ok && sh.den[t] > 0.0;
-                }
+                // the period owners' cap complementarity, primal residual and domain check ride
+                // along in the same reduction (a domain failure as an infinite dual residual: the
+                // merit is then non-finite and the loop stops, as before)
+                double mu, pr;
+                R.sum_max2(mu_l + own_rc4, own_bad ? __builtin_inf() : rd, own_pr, mu, rd, pr);
+                const double mu_sum = mu;   // c0 of the complementarity polynomial (cap terms included)
+                const bool domain_ok = true;
                 mu *= inv_ncon;
                 const double merit = fmax(mu, fmax(rd, pr));
                 min_pr = fmin(min_pr, pr);
@@ -1696,8 +1730,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                         sh.best_l1[gvt<GL>()] = l1t;
                     }
                     best_obj = 0.0;
-                } else if (best < 1e-6 && merit > 1e4 * best) {
-                    break;   // numerical breakdown after convergence: keep the best iterate
+                } else {
+                    if (best < 1e-6 && merit > 1e4 * best)
+                        break;   // numerical breakdown after convergence: keep the best iterate
                 }
                 if (mu < args.tol && rd < 10.0 * args.tol && pr < 10.0 * args.tol) break;
                 KMPC_PH(ph, 0);
@@ -1739,9 +1774,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     const double amax = max_step<HM, NWM>(T, sh, R, cc1, cc2);
                     if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
                     const double ap = fmin(1.0, amax);
-                    double comp = mu_assets + ap * (cc1 + ap * cc2);
-                    if (T.ht)
-                        for (int t = 0; t < H; ++t) comp += (sh.z4[t] + ap * sh.dz4[t]) * (sh.l4[t] + ap * sh.dl4[t]);
+                    const double comp = mu_sum + ap * (cc1 + ap * cc2);   // (cap terms in cc1, cc2: max_step)
                     double sg = comp * inv_ncon / mu;
                     sg = sg * sg * sg;
                     const double smu = sg * mu;
