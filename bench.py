@@ -47,6 +47,38 @@ F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_solve_pmc.json")
 
 
+def solve_flop_model(N: int, H: int) -> dict:
+    """Algorithmic f64 FLOPs of ONE interior-point iteration of the register solve (DESIGN §3.2,
+    "FLOP model"), for one window of N assets and H periods: the arithmetic the algorithm needs in
+    exact arithmetic, counted once per active (asset, period), a division or reciprocal as 1 flop,
+    a multiply-add as 2. Not counted: padding lanes, recomputation, iterative refinement (zero in
+    exact arithmetic), reduction trees beyond one add per summand. Per-phase terms:
+
+      residuals      22 / (asset, period): R.w, budget and cap sums, both dual rows, x.l
+      factor         26 / (asset, period): slack reciprocals, P, E, the tridiagonal LDL^T of Q,
+                     diag(Q^-1), the Schur generators alpha_t, eps_t
+      Gram           per asset: the 3H(3H+1)/2 entries of G, 2 flops each (one product of the
+                     semiseparable generators + its accumulation), and the Q^-1 columns
+                     (H(H+1)/2 products + H(H-1) differences for the v-type generators)
+      Schur LDL^T    (3H)^3 / 3 per window
+      Newton         2 solves x 48 / (asset, period) (right-hand side 10, s-elimination 7, two
+                     tridiagonal solves 10, Z^T x 7, Z q 6, direction + s back-substitution 8),
+                     plus 2 x 2 (3H)^2 per window for the triangular solves with L
+      step length    2 passes x 45 / (asset, period): dual directions 11, ratio tests 12,
+                     complementarity polynomial 21, m.dw 1
+      targets        20 / (asset, period): the corrector's x.l + dx.dl - sigma mu
+      update         21 / (asset, period): dual directions + five axpys
+    """
+    K = 3 * H
+    ap = N * H
+    per_ap = {"residuals": 22, "factor": 26, "newton": 2 * 48, "step_length": 2 * 45, "targets": 20, "update": 21}
+    phases = {k: v * ap for k, v in per_ap.items()}
+    phases["gram"] = N * (2 * K * (K + 1) // 2 + H * (H + 1) // 2 + H * (H - 1))
+    phases["schur_ldlt"] = K ** 3 // 3
+    phases["newton"] += 2 * 2 * K * K
+    return {"per_iteration": sum(phases.values()), "phases": phases}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -123,10 +155,12 @@ def window_inputs(lo: int, hi: int, N: int, obs: int, seed: int, device):
     return torch.cat(xs).contiguous(), torch.cat(ws).contiguous()
 
 
-def timed_loop(step, steps: int, warmup: int, world: int, device):
+def timed_loop(step, steps: int, warmup: int, world: int, device, info: dict = None):
     """The bench contract's timing: `warmup` untimed steps, then exactly `steps` steps bracketed by a
     barrier + device synchronize on both sides; the elapsed time is the MAX over ranks (all_reduce).
-    step(k) runs one step (k = None for warmup) and returns its output; returns (elapsed, last)."""
+    step(k) runs one step (k = None for warmup) and returns its output; returns (elapsed, last).
+    The warmup steps include the step's collective, so communicator setup is not timed.
+    info (optional) receives this rank's own elapsed time as "local_elapsed_s"."""
     import torch.distributed as dist
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
     out = None
@@ -144,6 +178,8 @@ def timed_loop(step, steps: int, warmup: int, world: int, device):
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    if info is not None:
+        info["local_elapsed_s"] = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -151,9 +187,51 @@ def timed_loop(step, steps: int, warmup: int, world: int, device):
     return elapsed, out
 
 
+def rank_provenance(windows: int, local_elapsed: float, device) -> dict:
+    """What the process group itself saw, for the N > 1 line (every rank must call this: it is one
+    all_gather): the backend, the group's world size, and each rank's window count and own timed
+    seconds — so a SCALE record proves from the line that RCCL ran N ranks over the whole batch."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    t = torch.tensor([float(windows), float(local_elapsed)], dtype=torch.float64, device=device)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return {"backend": str(dist.get_backend()), "world_size": world,
+            "windows_per_rank": [int(p[0].item()) for p in parts],
+            "rank_elapsed_s": [float(p[1].item()) for p in parts]}
+
+
+def check_world(world: int, gpus: int) -> None:
+    """bench.py --gpus N must run as exactly N ranks (torch.distributed.run, one rank per GPU)."""
+    if world != gpus:
+        sys.exit(f"bench.py --gpus {gpus} but the launch has WORLD_SIZE={world}: run one rank per GPU "
+                 f"under torch.distributed.run --nproc-per-node {gpus}")
+
+
+def torch_cpu_rollout(sd, x, H, N, mean_t, std_t):
+    """The reference's rollout ops (backtest.py:99-121 with model.py:756-797) batched over the
+    windows in torch on the CPU: encode, then H x (z @ K, full obs-width decode, slice the first N,
+    de-standardize)."""
+    with torch.no_grad():
+        z = x
+        for k in range(3):
+            z = torch.nn.functional.linear(z, sd[f"encoder.network.{2 * k}.weight"], sd[f"encoder.network.{2 * k}.bias"])
+            if k < 2:
+                z = torch.relu(z)
+        ys = []
+        for _ in range(H):
+            z = z @ sd["kmat"]
+            p_ = torch.nn.functional.linear(z, sd["decoder.network.0.weight"])
+            ys.append(p_[:, :N] * std_t + mean_t)
+        return torch.stack(ys, 1)
+
+
 def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg, budget_s):
-    """The oracle's CPU restatement (numpy fp32 rollout + OpenMP float64 IPM) timed on a bounded
-    sample of the same windows on this host's cores. Returns (cpu_baseline dict, parity dict)."""
+    """SURVEY §8(d) item 2, "all-cores batched": the reference's rollout ops batched in torch on the
+    CPU (torch_cpu_rollout, all host threads) + the OpenMP float64 C restatement of the solve
+    (oracle/kmpc_oracle.c), timed on a bounded sample of the same windows on this host's cores.
+    The numpy restatement of the rollout (oracle/rollout.py) is kept as a cross-check only.
+    Returns (cpu_baseline dict, parity dict)."""
     from oracle import rollout as orollout, solver as osolver
     spec = {"kind": "generic",
             "enc_w": [sd[f"encoder.network.{2 * k}.weight"].numpy() for k in range(3)],
@@ -161,23 +239,31 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
             "enc_act": "relu", "kmat": sd["kmat"].numpy(), "norm_fn": "id",
             "dec_w": [sd["decoder.network.0.weight"].numpy()], "dec_b": [None]}
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    mean_t, std_t = torch.tensor(mean), torch.tensor(std)
 
     def run(lo, hi):
-        x = x_gpu[lo:hi].cpu().numpy()
+        x = x_gpu[lo:hi].cpu()
         wp = wp_gpu[lo:hi].cpu().numpy()
         t0 = time.perf_counter()
-        y = orollout.rollout(spec, x, H, N, mean, std)
+        y = torch_cpu_rollout(sd, x, H, N, mean_t, std_t).numpy()
         W, st, obj, it = osolver.solve_batch(wp, y, cfg.cost_coeff, cfg.max_turnover, cfg.allow_short,
                                              max_iter=cfg.max_iter, tol=cfg.tol, precision="d")
         return time.perf_counter() - t0, y, W, st
 
-    dt, _, _, _ = run(0, 2 * cores)                        # calibration (+ warms BLAS / OpenMP)
-    per = dt / (2 * cores)
-    n = int(min(max(budget_s / max(per, 1e-6), 2 * cores), x_gpu.shape[0]))
-    dt, y, W, st = run(0, n)
+    try:
+        dt, _, _, _ = run(0, 2 * cores)                    # calibration (+ warms BLAS / OpenMP)
+        per = dt / (2 * cores)
+        n = int(min(max(budget_s / max(per, 1e-6), 2 * cores), x_gpu.shape[0]))
+        dt, y, W, st = run(0, n)
+    finally:
+        torch.set_num_threads(threads)
     base = {"value": n / dt, "unit": "windows/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} windows of rank 0's C3 batch: numpy fp32 rollout (oracle/rollout.py) + "
-                      f"OpenMP float64 IPM (oracle/kmpc_oracle.c, {cores} threads), {dt:.1f} s"}
+            "sample": f"first {n} windows of rank 0's C3 batch: batched torch-CPU rollout in the reference's "
+                      f"ops (full obs-width decode, {cores} threads) + OpenMP float64 IPM "
+                      f"(oracle/kmpc_oracle.c, {cores} threads), {dt:.1f} s"}
+    y_np = orollout.rollout(spec, x_gpu[:256].cpu().numpy(), H, N, mean, std)   # cross-check only
     # parity on the same inputs: the float64 oracle solve of the device's own yhat (256 windows),
     # and the rollout (numpy fp32 vs MFMA fp32) relative error over the timed sample
     k = min(256, n)
@@ -190,7 +276,8 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
     parity = {"windows": k, "oracle_optimal": int((sto <= 1).sum()),
               "max_abs_dW0": float(np.abs(W0 - Wo[:, 0]).max()),
               "max_abs_dobj": float(np.abs(vg - vo).max()), "max_abs_obj": float(np.abs(vo).max()),
-              "rollout_max_rel_err": float(np.abs(ynp - y).max() / np.abs(y).max())}
+              "rollout_max_rel_err": float(np.abs(ynp - y).max() / np.abs(y).max()),
+              "torch_cpu_vs_numpy_rollout_max_rel_err": float(np.abs(y[:256] - y_np).max() / np.abs(y_np).max())}
     return base, parity
 
 
@@ -426,13 +513,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    check_world(world, args.gpus)
     import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        check_world(dist.get_world_size(), args.gpus)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
@@ -470,7 +556,9 @@ def main():
             gather_rows(W0, G, world, rank, dst=0)    # the one RCCL collective
         return y, W0, st, val, its
 
-    elapsed, (y, W0, st, val, its) = timed_loop(step, args.steps, args.warmup, world, dev)
+    tinfo = {}
+    elapsed, (y, W0, st, val, its) = timed_loop(step, args.steps, args.warmup, world, dev, tinfo)
+    prov = rank_provenance(B, tinfo["local_elapsed_s"], dev) if world > 1 else None
 
     roll_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     solve_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -495,15 +583,28 @@ def main():
         # PMC passes (64 lanes x (ADD + MUL + TRANS + 2 FMA) per wave-instruction), scaled by the
         # active-lane fraction N / blockDim (an upper bound on useful work: wave 0's serial Schur
         # phases idle more lanes), against the f64 FMA peak measured on this part (profiles/).
-        util = None
+        # algorithmic f64 FLOPs (solve_flop_model x this run's mean iteration count) against the
+        # same measured peak: the fraction of the f64 ceiling the ALGORITHM achieves; the executed
+        # (PMC) figure beside it counts padding lanes, recomputation and refinement as work
+        iters_mean = float(its.float().mean().item())
+        fm = solve_flop_model(N, H)
+        alg = fm["per_iteration"] * iters_mean
+        peak = F64_VALU_PEAK
+        util = {"pipe": "f64 VALU", "algorithmic_f64_flops_per_window": alg,
+                "algorithmic_f64_flops_per_iteration": fm["per_iteration"],
+                "algorithmic_phases_per_iteration": fm["phases"], "mean_ipm_iterations": iters_mean,
+                "unit": "TFLOP/s"}
         if pmc and "f64_flops_per_window" in pmc:
             lanes = pmc.get("active_lane_fraction", N / (64 * -(-N // 64)))
             useful = pmc["f64_flops_per_window"] * lanes * B / (solve_ms * 1e-3)
             peak = pmc.get("f64_peak_flops", F64_VALU_PEAK)
-            util = {"pipe": "f64 VALU", "executed_f64_flops_per_window": pmc["f64_flops_per_window"],
-                    "active_lane_fraction": lanes, "achieved": useful / 1e12, "peak": peak / 1e12,
-                    "unit": "TFLOP/s", "frac": useful / peak, "peak_source": pmc.get("f64_peak_source", "spec"),
-                    "counts_from": os.path.relpath(PMC_JSON, ROOT)}
+            util.update({"executed_f64_flops_per_window": pmc["f64_flops_per_window"],
+                         "executed_over_algorithmic": pmc["f64_flops_per_window"] / alg,
+                         "active_lane_fraction": lanes, "achieved": useful / 1e12,
+                         "frac": useful / peak, "counts_from": os.path.relpath(PMC_JSON, ROOT)})
+        util.update({"algorithmic_achieved": alg * B / (solve_ms * 1e-3) / 1e12, "peak": peak / 1e12,
+                     "algorithmic_frac": alg * B / (solve_ms * 1e-3) / peak,
+                     "peak_source": pmc.get("f64_peak_source", "spec") if pmc else "spec"})
         roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
                                 + H * (L * L + L * N))
         c4 = world > 1
@@ -519,7 +620,8 @@ def main():
                                    f"[{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
                        "windows_per_gpu": B, "global_windows_per_step": G,
                        "parallelism": (f"windows sharded over {world} GPUs (contiguous blocks of one global "
-                                       f"stream), RCCL gather of W0 to rank 0" if c4 else "1 GPU, no collective")},
+                                       f"stream), RCCL gather of W0 to rank 0" if c4 else "1 GPU, no collective")}
+                      | ({"dist": prov} if prov else {}),
             "roofline": roof,
             "compute_utilization": util,
             # SURVEY.md §8(d)'s whole-path bound: compulsory bytes per window = obs (f32 N d) +

@@ -268,7 +268,8 @@ size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_des
 /* Human-readable text for a return code or (status + 100) for a per-problem status. */
 const char* kmpc_strerror(int code);
 
-/* Library version string. */
+/* Library version string, "kmpc <ABI> (gfx950)". ABI 0.2.0 appended kmpc_solve_desc.path and
+   kmpc_rollout_desc.latent_unfused: callers built against 0.1.0 must rebuild. */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

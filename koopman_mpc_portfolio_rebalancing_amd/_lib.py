@@ -37,6 +37,10 @@ EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace
 
 PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
 
+# ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
+# kmpc_rollout_desc.latent_unfused, so an older library would read them past its structs' end
+ABI_VERSION = "0.2.0"
+
 
 class KmpcError(RuntimeError):
     pass
@@ -121,6 +125,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_strerror.restype = ctypes.c_char_p
     L.kmpc_version.argtypes = []
     L.kmpc_version.restype = ctypes.c_char_p
+    ver = L.kmpc_version().decode()
+    if ver.split()[1:2] != [ABI_VERSION]:
+        raise KmpcError(f"{p} reports {ver!r}; these bindings need ABI {ABI_VERSION}: rebuild the library")
     if path is None:
         _lib = L
     return L

@@ -24,7 +24,7 @@ int check_solve(const kmpc_solve_desc* d) {
 
 extern "C" {
 
-const char* kmpc_version(void) { return "kmpc 0.1.0 (gfx950)"; }
+const char* kmpc_version(void) { return "kmpc 0.2.0 (gfx950)"; }
 
 const char* kmpc_strerror(int code) {
     switch (code) {

@@ -86,6 +86,22 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
 #pragma unroll
         for (int t = 0; t < HR; ++t)
             if (t < H) rm[t] = fmaxf(rm[t], __shfl_xor(rm[t], o));
+    // a period whose every R underflowed to 0 (yhat <= -103.97): R_t . w_t = 0 on the whole simplex
+    // and the reference's exp cone exp(u) <= R_t . w_t has no solution (cvxpy: infeasible) —
+    // infeasible and the fallback, as the interior-point kernels report it
+    bool flat0 = false;
+#pragma unroll
+    for (int t = 0; t < HR; ++t) flat0 |= t < H && !(rm[t] > 0.0f);
+    if (flat0) {
+        if (act)
+            for (int t = 0; t < tw; ++t) wout[(size_t)t * N + lane] = wpi;   // mpc.py:113-115
+        if (lane == 0) {
+            a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+            a.obj[b] = __builtin_nan("");
+            if (a.iters) a.iters[b] = 0;
+        }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < HR; ++t) cnt[t] = (t < H && act && R[t] == rm[t]) ? 1 : 0;
     for (int o = 32; o > 0; o >>= 1)
@@ -136,10 +152,18 @@ __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a
     int bad = !(isfinite(a.c) && isfinite(a.tau));
     for (int i = lane; i < N; i += 64) bad |= !isfinite(wp[i]);
     for (int k = lane; k < H * N; k += 64) bad |= !isfinite(np_expf(y[k]));
-    if (wsumi(bad)) {
+    // a period whose every R underflowed to 0: infeasible (see simplex_regs)
+    int zero = 0;
+    for (int t = 0; t < H; ++t) {
+        float rm = 0.0f;
+        for (int i = lane; i < N; i += 64) rm = fmaxf(rm, np_expf(y[(size_t)t * N + i]));
+        zero |= !(wmaxf(rm) > 0.0f);
+    }
+    bad = wsumi(bad);
+    if (bad || zero) {
         for (int k = lane; k < tw * N; k += 64) wout[k] = wp[k % N];   // mpc.py:113-115
         if (lane == 0) {
-            a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+            a.status[b] = bad ? KMPC_STATUS_SOLVER_ERROR : KMPC_STATUS_INFEASIBLE;
             a.obj[b] = __builtin_nan("");
             if (a.iters) a.iters[b] = 0;
         }

@@ -1074,6 +1074,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
             z = 0.0;
             W.sum_max(z, nf);
         }
+        // a period whose every R is 0: the reference's exp cone is infeasible (as ipm_kernel)
+        bool r_zero = false;
+        if (nf == 0.0) {
+            for (int t = 0; t < H; ++t) W.slot(t, W.act ? 1.0 + W.mload(t) : 0.0);
+            W.finish(H);
+            for (int t = 0; t < H; ++t) r_zero = r_zero || sh.tot[t] == 0.0;
+        }
         double sig = fmax(mx, a.c);
         if (!(sig > 0.0)) sig = 1.0;
         W.isig = 1.0 / sig;
@@ -1085,7 +1092,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         double best_obj = __builtin_nan("");
 
         if (nf == 0.0 && isfinite(a.c) && isfinite(a.tau)) {
-            if (a.allow_short && !hs) {
+            if (r_zero) {
+                status = KMPC_STATUS_INFEASIBLE;
+            } else if (a.allow_short && !hs) {
                 // no bounds and no turnover terms: unbounded unless every period is flat
                 for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.mload(t) : 0.0);
                 W.finish(H);

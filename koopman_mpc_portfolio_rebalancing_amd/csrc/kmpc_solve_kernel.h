@@ -1582,6 +1582,18 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
     if (T.act) finite = finite && isfinite(T.wpi);
     mx = R.max1(mx);
     const double nonfinite = R.max1(finite ? 0.0 : 1.0);
+    // a period whose every R underflowed to 0 (yhat <= -103.97): R_t . w_t = 0 on the whole simplex,
+    // and the reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy reports infeasible
+    // (sum of R >= 0 over the assets: zero iff every R is zero)
+    bool r_zero = false;
+    {
+        double rs[HM];
+#pragma unroll
+        for (int t = 0; t < HM; ++t) rs[t] = (T.act && t < H) ? 1.0 + T.m[t] : 0.0;
+        R.periods(rs);
+#pragma unroll
+        for (int t = 0; t < HM; ++t) r_zero = r_zero || (t < H && rs[t] == 0.0);
+    }
     double sig = fmax(mx, args.c);
     if (!(sig > 0.0)) sig = 1.0;
     T.sig = sig;
@@ -1596,7 +1608,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
     double best_obj = __builtin_nan("");
 
     if (nonfinite == 0.0 && isfinite(args.c) && isfinite(args.tau)) {
-        if (args.allow_short && !T.hs) {
+        if (r_zero) {
+            status = KMPC_STATUS_INFEASIBLE;
+        } else if (args.allow_short && !T.hs) {
             // no bounds and no turnover terms: unbounded unless every period is flat
             double msum[HM];
 #pragma unroll

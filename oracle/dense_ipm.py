@@ -83,7 +83,10 @@ def dense_ipm(w_prev, y, cost, tau, allow_short=False, iters=100, tol=1e-12):
     m = gross_returns(y) - 1.0  # log(R.w) == log(1 + m.w) on sum(w) = 1
     y = np.asarray(y, np.float64)
     H, N = y.shape
+    from scipy.linalg import lu_factor, lu_solve
+    from scipy.sparse import csr_matrix, diags
     G, h, A, b, cvec, nw = _build(wp, y, cost, tau, allow_short)
+    Gs = csr_matrix(G)        # (the KKT matrix below is still formed and factored densely)
     nx = G.shape[1]
     mi = G.shape[0]
     x = np.zeros(nx)
@@ -113,12 +116,13 @@ def dense_ipm(w_prev, y, cost, tau, allow_short=False, iters=100, tol=1e-12):
             converged = True
             break
         Wd = lam / z
-        M = Hf + G.T @ (Wd[:, None] * G)
+        M = Hf + (Gs.T @ diags(Wd) @ Gs).toarray()
         K = np.block([[M, A.T], [A, np.zeros((H, H))]])
+        lu = lu_factor(K)
 
         def solve(rc):
             rhs1 = -rd - G.T @ (Wd * rg + rc / z)
-            sol = np.linalg.solve(K, np.concatenate([rhs1, -rp]))
+            sol = lu_solve(lu, np.concatenate([rhs1, -rp]))
             dx, dnu = sol[:nx], sol[nx:]
             dlam = -Wd * (G @ dx + rg) - rc / z
             dz = G @ dx + rg

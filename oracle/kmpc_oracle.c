@@ -390,6 +390,7 @@ static void nresidual(ws_t* W, real* const* b, real* const* r) {
     }
 }
 
+/* dev statistic (tools/refine_stats.py): refinement steps per Newton solve, atomic under OpenMP */
 static long nref_total = 0, nsolve_total = 0;
 __attribute__((destructor)) static void refstat(void) {
     if (getenv("KMPC_ORACLE_REFSTAT") && nsolve_total) fprintf(stderr, "refines/solve %.3f over %ld solves\n", (double)nref_total / nsolve_total, nsolve_total);
@@ -408,12 +409,12 @@ static void newton(ws_t* W) {
     }
     lsolve(W, W->b);
     real* sol[7] = {W->dw, W->ds, W->dl1, W->dl2, W->dl3, W->dl4, W->dnu};
-    static double adapt = -1;   /* stop refining once ||r||_inf <= adapt ||b||_inf */
-    if (adapt < 0) adapt = getenv("KMPC_ORACLE_REFINE_RTOL") ? atof(getenv("KMPC_ORACLE_REFINE_RTOL")) : 1e-7;
+    const double adapt = 1e-7;   /* stop refining once ||r||_inf <= adapt ||b||_inf (the kernels' REFINE_RTOL) */
     real bn = 0;
     if (adapt > 0) {
         for (int j = 0; j < 7; ++j) { size_t n = j < 5 ? HN : (size_t)H; for (size_t k = 0; k < n; ++k) bn = RFMAX(bn, RFABS(W->b[j][k])); }
     }
+#pragma omp atomic
     nsolve_total++;
     for (int it = 0; it < W->n_refine; ++it) {
         for (int j = 0; j < 7; ++j) memcpy(W->sv[j], sol[j], sizeof(real) * (j < 5 ? HN : (size_t)H));
@@ -423,6 +424,7 @@ static void newton(ws_t* W) {
             for (int j = 0; j < 7; ++j) { size_t n = j < 5 ? HN : (size_t)H; for (size_t k = 0; k < n; ++k) rn = RFMAX(rn, RFABS(W->r[j][k])); }
             if (rn <= adapt * bn) break;
         }
+#pragma omp atomic
         nref_total++;
 
         lsolve(W, W->r);
@@ -522,7 +524,7 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
     if (finite && ws_init(&W, N, H) == 0) {
         W.N = N; W.H = H; W.K = 3 * H;
         W.hw = !allow_short; W.hs = (c > 0) || (tau > 0); W.ht = tau > 0;
-        W.n_refine = getenv("KMPC_ORACLE_REFINE") ? atoi(getenv("KMPC_ORACLE_REFINE")) : 3;
+        W.n_refine = 3;   /* the kernels' default (kmpc_solve_desc.n_refine = 0 -> 3) */
         real sig = c;
         for (int i = 0; i < N; ++i) W.wp[i] = wp[i];
         for (size_t k = 0; k < HN; ++k) {
@@ -531,6 +533,15 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
         }
         if (!(sig > 0)) sig = 1;
         W.sig = sig; W.c = c / sig; W.tau = tau;
+
+        /* a period whose every R is 0 (yhat <= -103.97 underflows np.exp): R_t . w_t = 0 on the
+           whole simplex and the reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy
+           reports infeasible (mpc.py:113: fallback, value None) */
+        for (int t = 0; t < H; ++t) {
+            int zero = 1;
+            for (int i = 0; i < N; ++i) zero &= W.m[t * N + i] == -1;
+            if (zero) { status = ST_INFEASIBLE; goto done; }
+        }
 
         if (allow_short && !W.hs) {
             /* no bounds and no turnover terms: unbounded unless every period is flat */
@@ -642,10 +653,8 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
                 if (W.ht) W.rc4[t] += W.dz4[t] * W.dl4[t] - sg * mu;
             }
             {   /* corrector refinement only once mu <= 1e-6, 1e-5 with shorting (the kernels'
-                   REFINE_MU / REFINE_MU_SHORT) */
-                static double refine_mu = -1;
-                if (refine_mu < 0) refine_mu = getenv("KMPC_ORACLE_REFINE_MU") ? atof(getenv("KMPC_ORACLE_REFINE_MU")) : 0;
-                const double rmu = refine_mu > 0 ? refine_mu : (W.hw ? 1e-6 : 1e-5);
+                   REFINE_MU / REFINE_MU_SHORT; fixed constants: the goldens depend on them) */
+                const double rmu = W.hw ? 1e-6 : 1e-5;
                 const int nr = W.n_refine;
                 if (mu > (real)rmu) W.n_refine = 0;
                 newton(&W);

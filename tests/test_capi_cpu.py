@@ -28,7 +28,7 @@ def test_library_exports_every_header_function():
     assert set(names) == set(_lib.EXPORTED_SYMBOLS)
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.kmpc_version().decode().startswith("kmpc")
+    assert lib.kmpc_version().decode().startswith(f"kmpc {_lib.ABI_VERSION} ")
     assert lib.kmpc_strerror(_lib.KMPC_OK).decode() == "ok"
     assert lib.kmpc_strerror(100 + 1).decode() == "optimal_inaccurate"
 

@@ -97,6 +97,13 @@ def test_status_and_fallback_semantics():
     # non-finite predictions
     W, st, obj, _ = solver.solve([0.5, 0.5], np.array([[np.nan, 0.0]], np.float32), 1e-3, 0.2)
     assert solver.STATUS_NAMES[st] == "solver_error" and np.array_equal(W, [[0.5, 0.5]])
+    # a period whose every R underflows to 0 (np.exp(yhat <= -103.97) == 0): R.w = 0 on the whole
+    # simplex, the reference's exp cone exp(u) <= R.w is infeasible
+    yz = np.array([[-110.0, -120.0, -105.0], [0.01, 0.0, 0.02]], np.float32)
+    for c, tau in ((0.0, 0.0), (1e-3, 0.2)):
+        W, st, obj, _ = solver.solve([0.3, 0.3, 0.4], yz, c, tau)
+        assert solver.STATUS_NAMES[st] == "infeasible" and np.array_equal(W, np.tile([0.3, 0.3, 0.4], (2, 1)))
+        assert np.isnan(obj)
     # shorting allowed, no cost, no cap: log utility unbounded
     W, st, obj, _ = solver.solve([0.5, 0.5], y, 0.0, 0.0, allow_short=True)
     assert solver.STATUS_NAMES[st] == "unbounded" and np.array_equal(W, [[0.5, 0.5]])

@@ -88,12 +88,20 @@ def _bench_worker(rank, world, port, out_path, G, N, obs):
     try:
         lo, hi = window_range(G, world, rank)
         step = _stub_step_factory(lo, hi, G, world, rank, N, obs)
-        elapsed, W0 = bench.timed_loop(step, 3, 1, world, torch.device("cpu"))
+        info = {}
+        elapsed, W0 = bench.timed_loop(step, 3, 1, world, torch.device("cpu"), info)
         # every rank holds the same max-over-ranks elapsed time
         t = torch.tensor([elapsed], dtype=torch.float64)
         ts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(ts, t)
         assert all(float(v) == elapsed for v in ts) and elapsed > 0
+        assert 0 < info["local_elapsed_s"] <= elapsed
+        # the N > 1 line's provenance: what the process group saw (bench.rank_provenance)
+        prov = bench.rank_provenance(hi - lo, info["local_elapsed_s"], torch.device("cpu"))
+        assert prov["backend"] == "gloo" and prov["world_size"] == world
+        assert prov["windows_per_rank"] == [b - a for a, b in (window_range(G, world, r) for r in range(world))]
+        assert sum(prov["windows_per_rank"]) == G
+        assert max(prov["rank_elapsed_s"]) <= elapsed and prov["rank_elapsed_s"][rank] == info["local_elapsed_s"]
         if rank == 0:
             np.save(out_path, W0.numpy())
         else:
@@ -118,3 +126,14 @@ def test_bench_sharded_path_equals_single_process(tmp_path):
     step1 = _stub_step_factory(0, G, G, 1, 0, N, obs)
     _, ref = bench.timed_loop(step1, 1, 0, 1, torch.device("cpu"))
     assert np.array_equal(np.load(out), ref.numpy())
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """bench.py --gpus N exits non-zero unless the launch (and the process group) has N ranks."""
+    import bench
+    bench.check_world(2, 2)
+    with pytest.raises(SystemExit) as e:
+        bench.check_world(1, 2)
+    assert e.value.code not in (0, None)
+    with pytest.raises(SystemExit):
+        bench.check_world(4, 2)

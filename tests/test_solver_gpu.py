@@ -51,6 +51,7 @@ def test_solver_matches_golden(path):
     # optimal everywhere; with shorting (w unbounded below, an ill-conditioned reduced system) a
     # float64 solver may stop at optimal_inaccurate — a status the reference accepts (mpc.py:113)
     # — and the objective bar below still applies to every window
+    print("statuses", os.path.basename(path), st.tolist())
     assert (st == 0).all() if not short else (st <= 1).all() and (st == 0).mean() >= 0.9, st
     for b in range(W.shape[0]):
         assert _feasible(W[b], g["w_prev"][b], tau, short), b
@@ -61,6 +62,23 @@ def test_solver_matches_golden(path):
         assert val[b] == pytest.approx(dense_ipm.reference_objective(W[b], g["w_prev"][b], g["yhat"][b], c), abs=1e-12)
     if c > 0 and not short:
         assert np.abs(W[:, 0] - g["W"][:, 0]).max() < 1e-3
+
+
+@pytest.mark.parametrize("name", ["mpc_cfg3_N100_H10.npz", "mpc_cfg5_N500_H20.npz", "mpc_cfg1_N10_H5.npz"])
+def test_device_solutions_are_certified_optimal(name):
+    """The device's own W, certified by weak duality (oracle/certificate.py: the LP-optimal dual z
+    for y = 1 / (R.w), no interior-point code): gap <= the objective parity bar 1e-6 + 1e-5 |f*|.
+    This is W-parity as distance to the optimal set: it holds wherever on the optimal face the
+    interior point stops, so it transfers to any solver that reaches the optimum (SCS included)."""
+    from oracle import certificate
+    g = np.load(os.path.join(GOLD, name))
+    c, tau, _ = g["config"]
+    W, st, val = _solve(g["w_prev"], g["yhat"], c, tau)
+    assert (st == 0).all()
+    for b in range(W.shape[0]):
+        r = certificate.certify(W[b], g["w_prev"][b], g["yhat"][b], c, tau)
+        assert r["violation"] <= 1e-8 and -1e-12 <= r["gap"] <= 1e-6 + 1e-5 * abs(r["f"]), (b, r)
+        assert -r["f"] == pytest.approx(val[b], abs=1e-12)
 
 
 def test_reference_test_mpc_cases_on_device():
@@ -280,6 +298,29 @@ def test_float32_gross_return_ties():
     assert st2[0] == 0 and sto2[0] == 0
     assert np.abs(W2[0, 0] - 0.5).max() < 1e-6 and np.abs(Wo2[0, 0] - 0.5).max() < 1e-6
     assert val2[0] == pytest.approx(np.log(np.float64(np.exp(a))), abs=1e-15)
+
+
+@pytest.mark.parametrize("N,H,c,tau,path", [(3, 2, 0.0, 0.0, 0),      # presolve, register fast path
+                                            (80, 20, 0.0, 0.0, 0),    # presolve, general loop
+                                            (3, 2, 1e-3, 0.2, 0),     # packed interior point
+                                            (100, 10, 1e-3, 0.2, 0),  # register kernel (C3 case)
+                                            (70, 7, 0.0, 0.0, 1),     # register kernel, no presolve
+                                            (300, 12, 1e-3, 0.2, 0)])  # large-window kernel
+def test_underflowed_period_is_infeasible(N, H, c, tau, path):
+    """R = np.exp(yhat) is 0 in float32 for yhat <= -103.97 (mpc.py:55). A period where every R is
+    0 has R.w = 0 on the whole simplex, and the reference's exp cone exp(u) <= R.w has no
+    solution: cvxpy reports infeasible, the strategy holds w_prev (mpc.py:113-115). Every path
+    reports it the same way as the oracle, next to an ordinary window."""
+    rng = np.random.default_rng(N + H)
+    wp = rng.dirichlet(np.ones(N), 2)
+    y = rng.normal(5e-4, 0.015, (2, H, N)).astype(np.float32)
+    y[1, H - 1, :] = -110.0
+    y[1, 0, 0] = -200.0
+    W, st, val = _solve(wp, y, c, tau, path=path)
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y, c, tau)
+    assert st[1] == 2 and sto[1] == 2, (st, sto)
+    assert np.array_equal(W[1], np.tile(wp[1], (H, 1))) and np.isnan(val[1])
+    assert st[0] == 0 and abs(val[0] - valo[0]) <= 1e-6 + 1e-5 * abs(valo[0])
 
 
 @pytest.mark.parametrize("N,H,B", [(30, 15, 1600), (300, 12, 1100)])

@@ -1,0 +1,160 @@
+"""GPU parity of the fused drop-in window (kmpc_window: rollout -> solve on one stream, one
+workspace) at the BASELINE shapes whose solve needs workspace, i.e. the large-window kernel.
+
+kmpc_window lays its workspace out as [rollout scratch | yhat | solve slabs] (kmpc_capi.hip).
+The solve slabs are only non-empty past 256 assets or 10 periods. These tests drive that layout
+through the strategy path the reference's loop calls (KoopmanMPCStrategy.rebalance_batch,
+reference backtest.py:80-131) and DeviceKoopman.window:
+
+* W0, status and value must equal rollout-then-solve (two separate C-ABI calls) bit for bit.
+* A sample must match the long-double oracle at the parity bar of test_solver_gpu.py: objective
+  within 1e-6 + 1e-5 |f*|, W0 within 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, KoopmanMPCStrategy,
+                                                   MPCConfig, solve_mpc_log_utility_batched)
+from oracle import rollout as R
+from oracle import solver as oracle
+
+pytestmark = pytest.mark.gpu
+
+
+class _Stats:
+    def __init__(self, mean, std):
+        self.mean, self.std = mean, std
+
+
+class _Dataset:
+    def __init__(self, data):
+        self.data = data
+
+    def __len__(self):
+        return self.data.shape[0]
+
+
+class WindowEnv:
+    """The slice of FinanceEnv that KoopmanMPCStrategy reads: test_dataset.data,
+    n_assets and the de-standardisation stats."""
+
+    def __init__(self, data, n_assets, mean, std):
+        self.test_dataset = _Dataset(data)
+        self.n_assets = n_assets
+        self.stats = _Stats(mean, std)
+
+
+def _oracle_sample(wp, y, idx, cfg):
+    Wo, sto, valo, _ = oracle.solve_batch(wp[idx], y[idx], cfg.cost_coeff, cfg.max_turnover, cfg.allow_short)
+    return Wo, sto, valo
+
+
+def _check_against_oracle(W0, st, val, wp, y, cfg, idx):
+    Wo, sto, valo = _oracle_sample(wp, y, idx, cfg)
+    assert (sto <= 1).all() and (st[idx] <= 1).all()
+    assert np.abs(val[idx] - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
+    assert np.abs(W0[idx] - Wo[:, 0]).max() < 1e-3
+
+
+def test_config5_strategy_window_equals_rollout_then_solve():
+    """BASELINE configs[4]: LISTAKM (linear encoder, 10 loops), 500 assets, latent 512, H = 20, bf16
+    MFMA rollout, large-window f64 solve. 600 windows exceed the kernel's 512 persistent slots, so
+    slabs are reused inside the workspace region that follows yhat."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, B = 500, 512, 20, 600
+    obs_n = N * 20
+    sd, lc = bench.make_lista_state_dict(obs_n, L, seed=2)
+    cfg_m = {"MODEL": {"MODEL_NAME": "LISTAKM", "NORM_FN": "id",
+                       "ENCODER": {"LISTA": {"ALPHA": 5e-3, "L": lc, "NUM_LOOPS": 10}}}}
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, cfg_m), dev, dtype="bf16")
+    x, wp = bench.window_inputs(0, B, N, obs_n, seed=4, device=dev)
+    mean = np.full(N, 5e-4, np.float64)
+    std = np.full(N, 0.015, np.float64)
+    env = WindowEnv(x, N, mean, std)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    strat = KoopmanMPCStrategy(km, cfg)
+    ts = np.arange(B)
+    W0, st, val = strat.rebalance_batch(ts, wp.cpu().numpy(), env, return_info=True)
+    # the same windows as two separate calls: rollout (yhat in its own tensor), then the solve
+    y = km.rollout(x, mean, std, H, N)
+    W0b, stb, valb = solve_mpc_log_utility_batched(wp, y, cfg)
+    assert np.array_equal(W0, W0b.cpu().numpy())
+    assert np.array_equal(st, stb.cpu().numpy())
+    assert np.array_equal(val, valb.cpu().numpy(), equal_nan=True)
+    assert (st == 0).all()
+    # fused window with yhat kept (the caller's tensor instead of the workspace region)
+    W0c, stc, valc, yc = km.window(x, wp, mean, std, N, cfg, keep_yhat=True)
+    assert torch.equal(yc, y) and np.array_equal(W0c.cpu().numpy(), W0)
+    assert np.array_equal(valc.cpu().numpy(), val, equal_nan=True)
+    _check_against_oracle(W0, st, val, wp.cpu().numpy(), y.cpu().numpy(), cfg, np.array([0, 511, 512, B - 1]))
+
+
+def test_fp32_window_n300_h12_equals_rollout_then_solve():
+    """fp32 GenericKM window at N = 300, H = 12 (large-window kernel, 700 windows past its 512
+    slots), with a ball-normalised latent and the yhat kept in the workspace."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, B, d, hidden = 300, 128, 12, 700, 4, 256
+    obs_n = N * d
+    sd = bench.make_state_dict(obs_n, L, hidden, seed=6)
+    cfg_m = {"MODEL": dict(bench.MODEL_CFG["MODEL"], NORM_FN="ball")}
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, cfg_m), dev)
+    x, wp = bench.window_inputs(0, B, N, obs_n, seed=7, device=dev)
+    mean = np.linspace(-1e-3, 1e-3, N).astype(np.float32)
+    std = np.linspace(0.01, 0.03, N).astype(np.float32)
+    cfg = MPCConfig(horizon=H, cost_coeff=2e-3, max_turnover=0.3)
+    W0, st, val = km.window(x, wp, mean, std, N, cfg)
+    y = km.rollout(x, mean, std, H, N)
+    W0b, stb, valb = solve_mpc_log_utility_batched(wp, y, cfg)
+    assert torch.equal(W0, W0b) and torch.equal(st, stb)
+    assert np.array_equal(val.cpu().numpy(), valb.cpu().numpy(), equal_nan=True)
+    assert (st.cpu().numpy() == 0).all()
+    # full W through the fused window equals the full solve as well
+    Wf, stf, _ = km.window(x[:64], wp[:64], mean, std, N, cfg, return_full=True)
+    Wfb, _, _ = solve_mpc_log_utility_batched(wp[:64], y[:64], cfg, return_full=True)
+    assert torch.equal(Wf, Wfb)
+    # the rollout itself against the numpy restatement
+    sdn = {k: v.numpy() for k, v in sd.items()}
+    spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
+               "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],
+               "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": "ball"}
+    ref = R.rollout(spec_np, x[:128].cpu().numpy(), H, N, mean, std)
+    yn = y[:128].cpu().numpy()
+    assert np.abs(yn - ref).max() <= 1e-4 * np.abs(ref).max()
+    _check_against_oracle(W0.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy(), wp.cpu().numpy(),
+                          y.cpu().numpy(), cfg, np.array([0, 512, B - 1]))
+
+
+def test_config0_model_rollout_and_window():
+    """BASELINE configs[0]'s exact model: finance_sparse GenericKM, 10 assets, obs 200, encoder
+    [1024, 1024], latent 128, H = 5 (the model of bench.cpu_baseline_c1 / secondary_c1). The GPU
+    rollout is checked against the numpy fp32 restatement on the bench's own windows. The fused
+    window (packed small-window solve, no solve workspace) is checked against rollout-then-solve
+    and against the oracle."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, hidden, B = 10, 128, 5, 1024, 4096
+    obs_n = N * 20
+    sd = bench.make_state_dict(obs_n, L, hidden, seed=10)
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), dev)
+    x, wp = bench.window_inputs(0, B, N, obs_n, seed=10, device=dev)
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    y = km.rollout(x, mean, std, H, N)
+    sdn = {k: v.numpy() for k, v in sd.items()}
+    spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
+               "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],
+               "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": "id"}
+    ref = R.rollout(spec_np, x.cpu().numpy(), H, N, mean, std)
+    yn = y.cpu().numpy()
+    assert yn.shape == (B, H, N)
+    assert np.abs(yn - ref).max() <= 1e-4 * np.abs(ref).max()
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    W0, st, val = km.window(x, wp, mean, std, N, cfg)
+    W0b, stb, valb = solve_mpc_log_utility_batched(wp, y, cfg)
+    assert torch.equal(W0, W0b) and torch.equal(st, stb) and torch.equal(val, valb)
+    assert (st.cpu().numpy() == 0).all()
+    _check_against_oracle(W0.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy(), wp.cpu().numpy(), yn, cfg,
+                          np.arange(0, B, 97))
