@@ -96,7 +96,7 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
         if (act)
             for (int t = 0; t < tw; ++t) wout[(size_t)t * N + lane] = wpi;   // mpc.py:113-115
         if (lane == 0) {
-            a.status[b] = KMPC_STATUS_SOLVER_ERROR;
+            a.status[b] = KMPC_STATUS_INFEASIBLE;
             a.obj[b] = __builtin_nan("");
             if (a.iters) a.iters[b] = 0;
         }

@@ -48,11 +48,9 @@ def test_solver_matches_golden(path):
     c, tau, short = g["config"]
     short = bool(short)
     W, st, val = _solve(g["w_prev"], g["yhat"], c, tau, short)
-    # optimal everywhere; with shorting (w unbounded below, an ill-conditioned reduced system) a
-    # float64 solver may stop at optimal_inaccurate — a status the reference accepts (mpc.py:113)
-    # — and the objective bar below still applies to every window
-    print("statuses", os.path.basename(path), st.tolist())
-    assert (st == 0).all() if not short else (st <= 1).all() and (st == 0).mean() >= 0.9, st
+    # optimal everywhere, the shorting golden included (pinned: every window reaches "optimal" since
+    # the shorting refinement threshold REFINE_MU_SHORT; a status regression fails here)
+    assert (st == 0).all(), st
     for b in range(W.shape[0]):
         assert _feasible(W[b], g["w_prev"][b], tau, short), b
     f_ref = g["obj"]
