@@ -79,6 +79,10 @@ struct BigArgs {
     int NP;          // padded asset count (blockDim)
 };
 
+// LDS of the fused solves: the raw Gram's v-columns, c_t = sqrt(rho_t) px_t, per-wave px partials
+template <int HM>
+constexpr int fx_doubles() { return KP * HM + HM + NWX * HM; }
+
 template <int HM>
 struct BigShared {
     double G[KP * LDG];          // Schur matrix (lower triangle), then L (unit lower, strictly below)
@@ -90,6 +94,8 @@ struct BigShared {
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     double rw[HM], best_rw[HM], best_l1[HM], px[HM], adw[HM], sds[HM], sdw[HM];
+    double isp1[HM];   // 1 / (1 + gamma SP), SP = sum_i P (rho = gamma isp1)
+    double pxa[HM];    // the direction's px summed over its solves: ds = P (DS - rho pxa), sum_i ds = pxa isp1
     int flag;
 };
 
@@ -137,6 +143,12 @@ struct Win {
     int sbuf;
     __amdgpu_buffer_rsrc_t rs;   // the slab (wave-uniform base and size)
     unsigned vo;                 // i * 8
+    // fused solves (>= 512-thread blocks): LDS block [Gv: KP x HM][cv: HM][pxr: NWX x HM] (fx_doubles);
+    // nullptr: the unfused right-hand-side sweep with its own px reduction
+    double* fx;
+    __device__ __forceinline__ double* gv() const { return fx; }
+    __device__ __forceinline__ double* cv() const { return fx + KP * HM; }
+    __device__ __forceinline__ double* pxr() const { return fx + KP * HM + HM; }
 
     __device__ __forceinline__ void bind(size_t slab_doubles) {
         rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, (int)(slab_doubles * sizeof(double)), 0x00020000);
@@ -228,6 +240,11 @@ struct Win {
         dl2 = hs() ? (-rc2 - e.l2 * (ds - dd)) * e.iz2 : 0.0;
         dl3 = hs() ? (-rc3 - e.l3 * (ds + dd)) * e.iz3 : 0.0;
     }
+    // ds of (t, i) from the stored DS (the back-substituted s right-hand sides summed over the
+    // direction's solves): ds = P (DS - rho pxa) — the s elimination's last step, never stored
+    __device__ __forceinline__ double dsv(int t, const St& e, double DSraw) const {
+        return hs() ? e.P * (DSraw - sh.rho[t] * sh.pxa[t]) : 0.0;
+    }
     __device__ __forceinline__ double alpha(int t, double m) const { return m * sh.iden[t] * irsig; }
     __device__ __forceinline__ double eps(int t, const St& e) const { return ht() ? sh.sr[t] * e.bma * e.P : 0.0; }
     __device__ __forceinline__ double epsa(int t) const { return ht() ? sh.sr[t] * at(A_BP, t) : 0.0; }
@@ -285,7 +302,7 @@ struct Win {
     // (ipm_kernel's corrector rows)
     __device__ __forceinline__ void corr_rc(int t, const St& e, const Pre& p, double dd, double smu,
                                             double& r1, double& r2, double& r3) const {
-        const double dw = p.dw, ds = p.ds;
+        const double dw = p.dw, ds = dsv(t, e, p.ds);
         double rc1, rc2, rc3;
         xl(e, rc1, rc2, rc3);
         double dl1, dl2, dl3;
@@ -418,8 +435,10 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
         const int t = threadIdx.x;
         const double st = t < H ? sh.tot[t] : 0.0;
         const double ga = (ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
-        sh.rho[t] = (ht && t < H) ? ga / (1.0 + ga * st) : 0.0;
+        const double i1 = 1.0 / (1.0 + ga * st);
+        sh.rho[t] = (ht && t < H) ? ga * i1 : 0.0;
         sh.sr[t] = sqrt(sh.rho[t]);
+        sh.isp1[t] = i1;
     }
     if (!ok) sh.flag = 1;
     W.sum_max(mu_l, rd);   // (its barrier publishes rho, sr and flag)
@@ -527,12 +546,21 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
 // Wave 0: G + I' = L D L^T in LDS (lane r owns row r; unused rows become identity). Right-looking:
 // step j scales column j and updates the trailing rows, one LDS read-modify-write per entry.
 template <int HM>
-__device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht) {
+__device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht, double* gv = nullptr) {
     if (threadIdx.x < WAVE) {
         const int K3 = 3 * H;
         const int r = threadIdx.x;
         const int ty = r % 3;
         const bool rused = r < K3 && (ty != 0 || ht);
+        // fused solves: the v-columns of Z^T Q^-1 Z (before I' and the factorization) for the s
+        // elimination's rank-one term, Gv[p][tau] = G[p][3 tau] (lower-triangle storage)
+        if (gv && ht && r < K3) {
+            for (int tau = 0; tau < H; ++tau) {
+                const int p = 3 * tau;
+                gv[r * HM + tau] = p <= r ? sh.G[r * LDG + p] : sh.G[p * LDG + r];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
         // assemble row r (lower triangle) with I' and identity rows
         if (r < K3) {
             for (int k = 0; k <= r; ++k) {
@@ -566,8 +594,11 @@ __device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht) 
 
 // Wave 0: q = G^{-1} rhs, rhs[3t + type] from sh.tot (type-major slots tot[type * H + t]),
 // budget rows minus lb6 -> sh.q
+// fx (fused solves, cap active): rhs += Gv c (the s elimination's rank-one term folded into the
+// Schur system), and the v components of q are returned as q - c
 template <int HM>
-__device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H) {
+__device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H, const double* gv = nullptr,
+                                            const double* cv = nullptr) {
     if (threadIdx.x < WAVE) {
         const int K3 = 3 * H;
         const int lane = threadIdx.x;
@@ -576,6 +607,8 @@ __device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H) {
             const int t = lane / 3, ty = lane - 3 * t;
             x = sh.tot[ty * H + t];
             if (ty == 2) x -= sh.lb6[t];
+            if (gv)
+                for (int tau = 0; tau < H; ++tau) x = fma(gv[lane * HM + tau], cv[tau], x);
         }
         // forward: L y = rhs (lane r reads row r of L), then D^{-1}
         const int lr = lane < K3 ? lane : 0;
@@ -589,6 +622,7 @@ __device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H) {
             const double qj = bcast(x, j);
             if (lane < j) x = fma(-sh.G[j * LDG + lr], qj, x);
         }
+        if (gv && lane < K3 && lane % 3 == 0) x -= cv[lane / 3];
         if (lane < K3) sh.q[lane] = x;
     }
     __syncthreads();
@@ -606,8 +640,90 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
+    // Fused (W.fx, cap active): the right-hand sides and the forward sweep of Q^-1 in ONE pass over
+    // the state. The s elimination's rank-one term needs px = sum_i P bs, a block sum; instead of a
+    // sweep of its own it is folded into the Schur system: with c_t = sqrt(rho_t) px_t,
+    //   x = Q^-1 (rhs_w - D(BP bs)) + Q^-1 Z_v c  (the v-columns of Z: eps_t (e_t - e_{t-1}), eps = sqrt(rho) BP)
+    // so Z^T x = Z^T x' + Gv c (Gv: the raw Gram's v-columns, kept by schur_factor) and
+    // dw = x' - Q^-1 Z (q - E_v c). px is summed in the same block reduction as Z^T x'.
+    const bool fused = W.fx != nullptr && ht;
+    if (fused) {
+        double y = 0.0;
+        St cur{};
+        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0, r0c = 0.0, r1c = 0.0;
+        // bs of period t from its state, targets (first) or refinement residual
+        auto bsv = [&](int t, const St& e, double rc2, double rc3, double r1) -> double {
+            const double b1 = first ? -(W.cs_c - (e.l2 + e.l3 - sh.l4[t])) : r1;
+            const double p23 = first ? -rc2 * e.iz2 - rc3 * e.iz3 : 0.0;
+            return b1 + p23 - sh.lb5[t] * sh.iz4[t];
+        };
+        double bsc = 0.0, gpc = 0.0;
+        if (W.act) {
+            const auto p = W.pre(0, corr, false, !first);
+            cur = W.st(p, W.wpi);
+            if (corr) {
+                dwc = p.dw;
+                W.corr_rc(0, cur, p, dwc, smu, rc1c, rc2c, rc3c);
+            } else if (first) {
+                W.xl(cur, rc1c, rc2c, rc3c);
+            }
+            r0c = p.r0;
+            r1c = p.r1;
+            bsc = bsv(0, cur, rc2c, rc3c, r1c);
+            gpc = cur.bma * cur.P * bsc;
+        }
+        for (int t = 0; t < H; ++t) {
+            double pxv = 0.0;
+            if (W.act) {
+                const bool nx = t + 1 < H;
+                St nxt = cur;
+                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0, r0n = 0.0, r1n = 0.0;
+                if (nx) {
+                    const auto p = W.pre(t + 1, corr, false, !first);
+                    nxt = W.st(p, cur.w);
+                    if (corr) {
+                        dwn = p.dw;
+                        W.corr_rc(t + 1, nxt, p, dwn - dwc, smu, rc1n, rc2n, rc3n);
+                    } else if (first) {
+                        W.xl(nxt, rc1n, rc2n, rc3n);
+                    }
+                    r0n = p.r0;
+                    r1n = p.r1;
+                }
+                double b0, p1 = 0.0, p2 = 0.0, p3 = 0.0, pn = 0.0;
+                if (first) {
+                    double rdw, rds;
+                    W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
+                    b0 = -rdw;
+                    p1 = hw ? -rc1c * cur.iw : 0.0;
+                    p2 = -rc2c * cur.iz2;
+                    p3 = -rc3c * cur.iz3;
+                    if (nx) pn = -rc3n * nxt.iz3 + rc2n * nxt.iz2;
+                    if (bn)
+                        *bn = fmax(*bn, fmax(fmax(fabs(rdw), fabs(rds)),
+                                             fmax(fabs(rc1c), fmax(fabs(rc2c), fabs(rc3c)))));
+                } else {
+                    b0 = r0c;
+                }
+                const double bw = b0 + p1 + (p3 - p2) - pn;
+                const double bsn = nx ? bsv(t + 1, nxt, rc2n, rc3n, r1n) : 0.0;
+                const double gpn = nx ? nxt.bma * nxt.P * bsn : 0.0;
+                y = (bw - gpc + gpn) + W.at(A_LR, t) * y;   // forward sweep of Q^-1 (Y)
+                W.at(A_Y, t) = y;
+                W.at(A_BS, t) = bsc;
+                pxv = cur.P * bsc;
+                cur = nxt;
+                rc1c = rc1n; rc2c = rc2n; rc3c = rc3n;
+                dwc = dwn; r0c = r0n; r1c = r1n;
+                bsc = bsn;
+                gpc = gpn;
+            }
+            pxv = wave_sum(pxv);   // (every lane of the wave: outside the divergent branch)
+            if ((threadIdx.x & (WAVE - 1)) == 0) W.pxr()[(threadIdx.x / WAVE) * HM + t] = pxv;
+        }
+    }
     // ---- A: right-hand sides (BW, BS) and px = sum_i P bs ----
-    {
+    if (!fused) {
         // per period: the raw state, the affine direction (corr), the targets (first) or the
         // refinement residual (!first)
         St cur{};
@@ -682,7 +798,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     }
     // ---- B: s elimination, x = Q^{-1} rhs_w (X), Schur rhs Z^T x, q = G^{-1} (...) ----
     {
-        if (W.act) {
+        if (W.act && !fused) {
             // rhs_w -= g_t - g_{t+1}, g = bma P (bs - rho px); forward sweep y_t = x_t + Lr_t y_{t-1} (Y)
             double y = 0.0;
             double gc = hs ? W.at(A_BP, 0) * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
@@ -716,7 +832,21 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             epn = ep;
         }
         W.finish(3 * H);
-        schur_solve(sh, H);
+        if (fused) {
+            // px of this solve (the per-wave partials of the fused sweep, published by finish's
+            // barrier) and c = sqrt(rho) px, on wave 0 (schur_solve's wave: no barrier between)
+            if (threadIdx.x < HM) {
+                const int t = threadIdx.x;
+                double px = 0.0;
+                if (t < H)
+                    for (int q = 0; q < W.nw; ++q) px += W.pxr()[q * HM + t];
+                sh.px[t] = px;
+                W.cv()[t] = sh.sr[t] * px;
+            }
+            schur_solve(sh, H, W.gv(), W.cv());
+        } else {
+            schur_solve(sh, H);
+        }
     }
     // ---- C: dw = x - Q^{-1} (Z q) (DW), bs -= bma dd (BS), px = sum_i P bs ----
     {
@@ -744,14 +874,16 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 const double dw = W.at(A_X, t) - tq;
                 if (first) W.at(A_DW, t) = dw; else W.at(A_DW, t) += dw;
                 const double bma = hs ? W.at(A_BMA, t) : 0.0, P = hs ? W.at(A_P, t) : 0.0;
+                // the back-substituted s right-hand side goes to DS (summed over the solves);
+                // ds = P (DS - rho pxa) is formed where it is read (Win::dsv)
                 if (hs && t + 1 < H) {
                     const double bs = W.at(A_BS, t + 1) - bman * (dwn - dw);
-                    W.at(A_BS, t + 1) = bs;
+                    if (first) W.at(A_DS, t + 1) = bs; else W.at(A_DS, t + 1) += bs;
                     pxn = Pn * bs;
                 }
                 if (hs && t == 0) {
                     const double bs = W.at(A_BS, 0) - bma * dw;
-                    W.at(A_BS, 0) = bs;
+                    if (first) W.at(A_DS, 0) = bs; else W.at(A_DS, 0) += bs;
                     px0 = P * bs;
                 }
                 dwn = dw;
@@ -763,18 +895,14 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         }
         W.finish(H);
     }
-    // ---- D: ds = P (bs - rho px) (DS); budget multipliers ----
+    // ---- D: px summed over the solves (ds = P (DS - rho pxa)); budget multipliers ----
     {
-        if (W.act) {
-            for (int t = 0; t < H; ++t) {
-                const double ds = hs ? W.at(A_P, t) * (W.at(A_BS, t) - sh.rho[t] * sh.tot[t]) : 0.0;
-                if (first) W.at(A_DS, t) = ds; else W.at(A_DS, t) += ds;
-            }
-        }
         if (threadIdx.x < HM) {
             const int t = threadIdx.x;
             const double dn = t < H ? sh.q[3 * t + 2] : 0.0;
             sh.dnu[t] = first ? dn : sh.dnu[t] + dn;
+            const double px = (hs && t < H) ? sh.tot[t] : 0.0;
+            sh.pxa[t] = first ? px : sh.pxa[t] + px;
         }
         __syncthreads();
     }
@@ -808,23 +936,21 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
         if (r >= n_refine) break;
         // residual of rows (1), (2), (7) of the direction; rows (3)-(6) hold by construction
         for (int t = 0; t < H; ++t) {
-            double va = 0.0, vs = 0.0, vw = 0.0;
+            double va = 0.0, vw = 0.0;
             if (W.act) {
                 vw = W.at(A_DW, t);
                 va = W.alpha(t, W.mload(t)) * vw;
-                vs = W.at(A_DS, t);
             }
             W.slot(t, va);
-            W.slot(H + t, vs);
-            W.slot(2 * H + t, vw);
+            W.slot(H + t, vw);
         }
-        W.finish(3 * H);
+        W.finish(2 * H);
         if (threadIdx.x < HM) {
             const int t = threadIdx.x;
             const bool on = t < H;
             sh.adw[t] = on ? sh.tot[t] : 0.0;
-            sh.sds[t] = on ? sh.tot[H + t] : 0.0;
-            sh.sdw[t] = on ? sh.tot[2 * H + t] : 0.0;
+            sh.sds[t] = (on && hs) ? sh.pxa[t] * sh.isp1[t] : 0.0;   // sum_i ds (no sweep)
+            sh.sdw[t] = on ? sh.tot[H + t] : 0.0;
         }
         __syncthreads();
         double rn = 0.0;
@@ -832,7 +958,7 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
             double nl2 = 0.0, nl3 = 0.0, l2n = 0.0, l3n = 0.0;   // dl2 / dl3 / l2 / l3 of period t + 1
             for (int t = H - 1; t >= 0; --t) {
                 const St e = W.st(t, W.wprev(t));
-                const double dw = W.at(A_DW, t), ds = W.at(A_DS, t);
+                const double dw = W.at(A_DW, t), ds = W.dsv(t, e, W.at(A_DS, t));
                 const double dd = dw - (t ? W.at(A_DW, t - 1) : 0.0);
                 double dl1, dl2, dl3;
                 W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
@@ -861,13 +987,11 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
         }
         __syncthreads();
     }
-    // dz4 / dl4 of the final direction
-    for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.at(A_DS, t) : 0.0);
-    W.finish(H);
+    // dz4 / dl4 of the final direction: sum_i ds = pxa / (1 + gamma SP) (no sweep)
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
         const bool on = ht && t < H;
-        const double st = t < H ? sh.tot[t] : 0.0;
+        const double st = (hs && t < H) ? sh.pxa[t] * sh.isp1[t] : 0.0;
         sh.dz4[t] = on ? -st + sh.rg4[t] : 0.0;
         sh.dl4[t] = on ? (sh.b5[t] + sh.l4[t] * st) * sh.iz4[t] : 0.0;
     }
@@ -895,7 +1019,7 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
             if (t + 1 < H) pn = W.pre(t + 1, true, !pred);
             const St e = W.st(p, wprev);
             wprev = e.w;
-            const double dw = p.dw, ds = p.ds, dd = dw - dwp;
+            const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
             double r1 = p.rc1, r2 = p.rc2, r3 = p.rc3;
             if (pred) W.xl(e, r1, r2, r3);
@@ -952,7 +1076,7 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
             if (t + 1 < H) pn = W.pre(t + 1);
             const St e = W.st(p, wprev);
             wprev = e.w;
-            const double dw = p.dw, ds = p.ds, dd = dw - dwp;
+            const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
             W.ddirs(e, p.rc1, p.rc2, p.rc3, dw, ds, dd, dl1, dl2, dl3);
@@ -1013,7 +1137,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         if (mu < a.tol && rd < 10.0 * a.tol && pr < 10.0 * a.tol) break;
         if (sh.flag) break;   // Q not positive definite
         ph_gram(W);
-        schur_factor(sh, H, W.ht());
+        schur_factor(sh, H, W.ht(), W.fx ? W.gv() : nullptr);
         if (sh.flag) break;
         double step = 0.0, smu = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
@@ -1044,6 +1168,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                   (int)threadIdx.x, (int)threadIdx.x < a.N};
     W.bind(A.slab);
     W.sbuf = 0;
+#ifndef KMPC_BIG_FUSE
+#define KMPC_BIG_FUSE 1
+#endif
+    // fused solves on the >= 512-thread blocks (two per CU: the extra 13.6 KB fits; the 256-thread
+    // blocks run three per CU at the LDS limit and keep the unfused sweeps)
+    __shared__ double fxs[(KMPC_BIG_FUSE && MAXT >= 512) ? fx_doubles<HM>() : 1];
+    W.fx = (KMPC_BIG_FUSE && MAXT >= 512) ? fxs : nullptr;
     W.cs.set_case(!a.allow_short, (a.c > 0.0) || (a.tau > 0.0), a.tau > 0.0);
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int N = a.N, H = a.H, i = threadIdx.x;
