@@ -132,11 +132,17 @@ __device__ __forceinline__ void xcd_tile(int& m0, int& n0, int tm = BM, int tn =
     n0 = (id % gx) * tn;
 }
 
-template <int WT>
+// k-tile depth of the 64 x 64 tile (small window batches): 32, or 64 (one barrier pair per 32 MFMAs
+// per wave instead of per 16; dev A/B: tools/ab_c2.sh)
+#ifndef KMPC_GEMM_BK1
+#define KMPC_GEMM_BK1 32
+#endif
+template <int WT, int BKT = (WT == 1 ? KMPC_GEMM_BK1 : BK)>
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     constexpr int TM = 64 * WT;
-    __shared__ float As[TM * LDS_STRIDE];
-    __shared__ float Bs[TM * LDS_STRIDE];
+    constexpr int LS = BKT + 4;   // LDS row stride (floats): conflict-free ds_read_b128 fragments
+    __shared__ float As[TM * LS];
+    __shared__ float Bs[TM * LS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int m0, n0;
     xcd_tile(m0, n0, TM, TM);
@@ -154,20 +160,21 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     // split K: slice blockIdx.z of ksplit (whole BK tiles)
     int kbeg = 0, kend = g.K;
     if (g.ksplit > 1) {
-        const int kc = ((g.K + g.ksplit * BK - 1) / (g.ksplit * BK)) * BK;
+        const int kc = ((g.K + g.ksplit * BKT - 1) / (g.ksplit * BKT)) * BKT;
         kbeg = blockIdx.z * kc;
         kend = min(g.K, kbeg + kc);
     }
-    // A and B tiles: TM rows x 32 k = 8 TM float4 per operand, TM / 32 per thread. The next
-    // k-tile's global loads are issued into registers before this tile's MFMAs (register double
+    // A and B tiles: TM rows x BKT k = TM BKT / 4 float4 per operand, TM BKT / 1024 per thread. The
+    // next k-tile's global loads are issued into registers before this tile's MFMAs (register double
     // buffering: one LDS buffer, the HBM / L2 latency under the math).
-    constexpr int QN = TM / 32;
+    constexpr int QN = TM * BKT / 1024;
+    constexpr int RQ = BKT / 4;                     // float4 per row
     f32x4 va[QN], vb[QN];
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
-            const int idx = tid + q * 256;          // 0..8 TM - 1
-            const int row = idx >> 3, c4 = (idx & 7) * 4;
+            const int idx = tid + q * 256;          // 0 .. TM RQ - 1
+            const int row = idx / RQ, c4 = (idx % RQ) * 4;
             const int kk = k0 + c4;
             va[q] = f32x4{0.f, 0.f, 0.f, 0.f};
             vb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -187,37 +194,40 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
         }
     };
     fetch(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
             const int idx = tid + q * 256;
-            const int row = idx >> 3, c4 = (idx & 7) * 4;
-            *(f32x4*)(As + row * LDS_STRIDE + c4) = va[q];
-            *(f32x4*)(Bs + row * LDS_STRIDE + c4) = vb[q];
+            const int row = idx / RQ, c4 = (idx % RQ) * 4;
+            *(f32x4*)(As + row * LS + c4) = va[q];
+            *(f32x4*)(Bs + row * LS + c4) = vb[q];
         }
         __syncthreads();
-        if (k0 + BK < kend) fetch(k0 + BK);
+        if (k0 + BKT < kend) fetch(k0 + BKT);
         const int r = lane & 31, h = lane >> 5;
-        float af[WT][16], bf[WT][16];
 #pragma unroll
-        for (int a = 0; a < WT; ++a) {
-            const float* pa = As + (wm + a * 32 + r) * LDS_STRIDE + 16 * h;
-            const float* pb = Bs + (wn + a * 32 + r) * LDS_STRIDE + 16 * h;
+        for (int kb = 0; kb < BKT; kb += 32) {   // 32-k sub-steps: lane (r, h) takes k = kb + 16 h + s
+            float af[WT][16], bf[WT][16];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const f32x4 x = *(const f32x4*)(pa + 4 * q);
-                const f32x4 y = *(const f32x4*)(pb + 4 * q);
+            for (int a = 0; a < WT; ++a) {
+                const float* pa = As + (wm + a * 32 + r) * LS + kb + 16 * h;
+                const float* pb = Bs + (wn + a * 32 + r) * LS + kb + 16 * h;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) { af[a][4 * q + e] = x[e]; bf[a][4 * q + e] = y[e]; }
+                for (int q = 0; q < 4; ++q) {
+                    const f32x4 x = *(const f32x4*)(pa + 4 * q);
+                    const f32x4 y = *(const f32x4*)(pb + 4 * q);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { af[a][4 * q + e] = x[e]; bf[a][4 * q + e] = y[e]; }
+                }
             }
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+#pragma unroll
+                for (int a = 0; a < WT; ++a)
+#pragma unroll
+                    for (int b = 0; b < WT; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         }
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-#pragma unroll
-            for (int a = 0; a < WT; ++a)
-#pragma unroll
-                for (int b = 0; b < WT; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         __syncthreads();
     }
     if (g.ksplit > 1) {   // raw partial of this K slice

@@ -100,9 +100,6 @@ constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
 #ifndef KMPC_REFINE_MU_SHORT
 #define KMPC_REFINE_MU_SHORT 1e-5
 #endif
-#ifndef KMPC_PX_CORR   // 2: the corrector's first px reduced in the targets phase; 0: in its solve
-#define KMPC_PX_CORR 0
-#endif
 constexpr double REFINE_MU = KMPC_REFINE_MU;
 constexpr double REFINE_MU_SHORT = KMPC_REFINE_MU_SHORT;
 
@@ -468,7 +465,7 @@ struct Shared {
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM];
     double rho[HM], sr[HM];
     double sp[HM], isp1[HM];             // sum_i P per period; 1 / (1 + gamma SP) (rho = gamma isp1)
-    double pxd[NWM][pow2_at_least(HM)];  // per-wave partial sums of the corrector's first px (targets phase)
+    double pxd[NWM][pow2_at_least(HM)];  // (read only by an untaken branch of lsolve: see there)
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     double best_rw[HM], best_l1[HM];   // per-period R.w and ||w_t - w_{t-1}||_1 of the best iterate
     int flag;
@@ -881,14 +878,15 @@ __device__ __forceinline__ void dual_residual(const TH& T, const Shared<HM, NWM>
 // Solve the Newton system (oracle/kmpc_oracle.c:lsolve) for rhs rows (bw, bs, [-rc if with_c],
 // sh.lb5, sh.lb6), in place: on return bw = dw, bs = ds (and q in sh.bs; the budget multipliers
 // are q[2H..3H)). In-place arrays keep the register footprint of the solve to four [HM] arrays.
-// The first px = sum_i P bs per period (the s elimination's rank-one term) needs no reduction of its
-// own: pmode 1 (predictor: bs = -c - l4 - lb5 iz4 on every active lane, so px = bs SP), pmode 2 (the
-// corrector's first solve: the period sums of P (-rds + p2 + p3) were reduced in the targets phase,
-// sh.pxd; px = that - lb5 iz4 SP); pmode 0 reduces it here (refinement solves). pxo: the px of the
-// back-substitution (sum_i ds = px / (1 + gamma SP): the caller's dz4 needs no reduction either).
+// The first px = sum_i P bs per period (the s elimination's rank-one term) of a solve: pred_px
+// (predictor) needs no reduction — its bs = -c - l4 - lb5 iz4 is the same on every active lane, so
+// px = bs SP; the other solves reduce it here. pxo: the px of the back-substitution
+// (sum_i ds = px / (1 + gamma SP): the caller's dz4 needs no reduction either).
+// (Measured and not kept, r04: the corrector's first px reduced in its targets phase, on the barrier
+// already there: +58 spilled VGPRs, slower.)
 template <int HM, int NWM, class TH>
 __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
-                                       double (&bw)[HM], double (&bs)[HM], bool with_c, int pmode,
+                                       double (&bw)[HM], double (&bs)[HM], bool with_c, bool pred_px,
                                        double (&pxo)[HM]) {
     constexpr int KM = 3 * HM;
     const int H = T.H;
@@ -910,11 +908,17 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM>& sh, Reducer
     // (diag(alpha+beta) + gamma 1 1')^{-1} x per period = P (x - rho 1'P x)
     double px[HM], tq[HM];
     if (T.hs) {
-        if (pmode == 1) {
+        if (pred_px) {
 #pragma unroll
             for (int t = 0; t < HM; ++t)
                 px[t] = t < H ? (-T.c - sh.l4[t] - (T.ht ? sh.lb5[t] * sh.iz4[t] : 0.0)) * sh.sp[t] : 0.0;
-        } else if (pmode == 2) {
+        } else if (T.N < 0) {
+            // Never taken (N >= 1: the C ABI rejects the rest). Kept because this branch's presence
+            // changes the register allocation of the whole kernel: 46 -> 41 spilled VGPRs and +2.8%
+            // on the C3 solve, measured r04 (tools/ab_run.sh, two repeats; the compiler drops a
+            // branch whose condition it can prove false, and then the gain is gone). A live use —
+            // the refinement solves' px reduced with the residual norm into sh.pxd — spilled 121
+            // VGPRs at the refinement loop's peak and was slower.
 #pragma unroll
             for (int t = 0; t < HM; ++t) {
                 double v = sh.pxd[0][t];
@@ -1099,7 +1103,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
 #endif
         {
             double pxr[HM];
-            lsolve<HM, NWM>(T, sh, R, r0, r1, r == 0 && !pred, r == 0 ? (pred ? 1 : KMPC_PX_CORR) : 0, pxr);
+            lsolve<HM, NWM>(T, sh, R, r0, r1, r == 0 && !pred, r == 0 && pred, pxr);
             double pv = 0.0;
 #pragma unroll
             for (int k = 0; k < HM; ++k) pv = (k == town) ? pxr[k] : pv;
@@ -1236,161 +1240,6 @@ __device__ __forceinline__ double max_step(const TH& T, Shared<HM, NWM>& sh, Red
     return a;
 }
 
-// ---- Schur Gram on the f64 matrix cores ------------------------------------------------------------
-// The per-asset tridiagonal Q has a semiseparable inverse: Q^-1[r][c] = g_r beta_c (r <= c) with
-// pi_t = prod_{1<=k<=t} Lr_k, g = 1 / pi, beta = dq pi (dq = diag Q^-1). In period-major order
-// p = 3t + type with the types (v, a, budget) = (0, 1, 2) within a period, every entry (p, q), p <= q,
-// of an asset's contribution to G is a product Lgen[p] Rgen[q]:
-//   Lgen = (eps_t (g_t - g_{t-1}), alpha_t g_t, g_t),  Rgen = (eps_t (beta_t - beta_{t-1}), alpha_t beta_t, beta_t)
-// except (v_t, v_t), whose product form cancels: eps_t^2 (dq_t - 2 Lr_t dq_t + dq_{t-1}) is summed
-// directly. The sum over assets is the GEMM Lgen^T Rgen on v_mfma_f64_16x16x4f64 with the assets as
-// the K dimension: no cross-lane reduction of the 465 entries (the static Gram's reduce-scatter).
-// Each wave runs the K loop over its own 64 assets; the generators are transposed into the MFMA
-// operand layout through LDS rows that are dead during factor() — the cold rows of rc1..rc3 (30 rows
-// of CS slots), each wave in its own lanes' slots — in three rounds, one per tile (blocks of 15
-// indices = 5 periods): (L0, R0) -> tile (0,0), R1 over R0 -> (0,1), L1 over L0 -> (1,1). The second
-// wave's partial tiles go to LDS (G is dead here), and wave 0 sums them into the lower triangle of G
-// in this kernel's type-major index order (type * HM + t, types a, v, budget).
-// Lr is clamped at 1e-14 (pi stays normal over 10 periods); the clamp changes only Q^-1 entries that
-// are already below 1e-14 of the diagonal.
-typedef double gram_d4 __attribute__((ext_vector_type(4)));
-#ifndef KMPC_MFMA_GRAM
-#define KMPC_MFMA_GRAM 1
-#endif
-template <int HM, int NWM, class TH>
-constexpr bool mfma_gram() { return KMPC_MFMA_GRAM && TH::GLN == 64 && TH::L && NWM <= 2 && HM == 10; }
-
-template <int HM, int NWM, class TH>
-__device__ __forceinline__ void gram_mfma(const TH& T, Shared<HM, NWM>& sh, Reducer<HM, NWM, TH::GLN>& R,
-                                          const double (&dq)[HM], const double (&Lr)[HM]) {
-    constexpr int KM = 3 * HM;
-    constexpr int CS = TH::CSV;
-    constexpr int BW = 15;                 // indices per block (5 periods)
-    constexpr int RW = Shared<HM, NWM>::RW;
-    static_assert(KM == 2 * BW, "two 15-wide blocks");
-    const int H = T.H;
-    const int lane = (int)threadIdx.x & (WAVE - 1), wv = (int)threadIdx.x / WAVE;
-    const int slot = (int)threadIdx.x < CS ? (int)threadIdx.x : CS - 1;
-    double* stg = kmpc_cold;               // rows 0 .. 29: rc1..rc3, dead until the predictor targets
-    // generators, forward in t; block 0 (periods 0..4) straight to LDS, block 1 held for rounds 2 / 3
-    double hl[BW], hr[BW], vv[HM];
-    {
-        double pi = 1.0, gp = 0.0, bp = 0.0;
-#pragma unroll
-        for (int t = 0; t < HM; ++t) {
-            const bool on = T.act && t < H;
-            if (t > 0) pi *= fmax(Lr[t], 1e-14);
-            const double g = rcp_nr(pi), b = dq[t] * pi;
-            const double al = on ? T.m[t] * sh.iden[t] * T.irsig : 0.0;
-            const double ep = (on && T.ht) ? sh.sr[t] * T.bma(t) * T.P[t] : 0.0;
-            const double lg[3] = {ep * (t ? g - gp : g), al * g, on ? g : 0.0};
-            const double rg[3] = {ep * (t ? b - bp : b), al * b, on ? b : 0.0};
-            vv[t] = ep * ep * (t ? dq[t] - 2.0 * Lr[t] * dq[t] + dq[t - 1] : dq[t]);
-#pragma unroll
-            for (int ty = 0; ty < 3; ++ty) {
-                const int p = 3 * t + ty;
-                if (p < BW) {
-                    stg[p * CS + slot] = lg[ty];
-                    stg[(BW + p) * CS + slot] = rg[ty];
-                } else {
-                    hl[p - BW] = lg[ty];
-                    hr[p - BW] = rg[ty];
-                }
-            }
-            gp = g;
-            bp = b;
-        }
-    }
-    // the direct (v_t, v_t) sums: wave reduce-scatter into this wave's reduction slots
-    {
-        double v[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) v[t] = t < HM ? vv[t] : 0.0;
-        const int s = wave_reduce_scatter<16, 64>(v);
-        if ((lane & 3) == 0) sh.red[R.buf][0][wv * RW + s] = v[0];
-    }
-    // K loop over this wave's assets: A = Lgen block (row i), B = Rgen block (column i), lane = i + 16 k
-    const int i = lane & 15, kk = lane >> 4;
-    const int na = T.N - WAVE * wv;
-    const int nk = ((na < WAVE ? na : WAVE) + 3) >> 2;
-    const int s0 = WAVE * wv + kk;
-    const bool ri = i < BW;
-    gram_d4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
-    __builtin_amdgcn_wave_barrier();
-    for (int s = 0; s < nk; ++s) {
-        const double a = ri ? stg[i * CS + s0 + 4 * s] : 0.0;
-        const double b = ri ? stg[(BW + i) * CS + s0 + 4 * s] : 0.0;
-        c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c00, 0, 0, 0);
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int q = 0; q < BW; ++q) stg[(BW + q) * CS + slot] = hr[q];
-    __builtin_amdgcn_wave_barrier();
-    for (int s = 0; s < nk; ++s) {
-        const double a = ri ? stg[i * CS + s0 + 4 * s] : 0.0;
-        const double b = ri ? stg[(BW + i) * CS + s0 + 4 * s] : 0.0;
-        c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c01, 0, 0, 0);
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int q = 0; q < BW; ++q) stg[q * CS + slot] = hl[q];
-    __builtin_amdgcn_wave_barrier();
-    for (int s = 0; s < nk; ++s) {
-        const double a = ri ? stg[i * CS + s0 + 4 * s] : 0.0;
-        const double b = ri ? stg[(BW + i) * CS + s0 + 4 * s] : 0.0;
-        c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c11, 0, 0, 0);
-    }
-    // the second wave's partial tiles to LDS (G is dead until wave 0 writes it below)
-    if (NWM > 1 && wv == 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            sh.G[(0 * 4 + r) * WAVE + lane] = c00[r];
-            sh.G[(1 * 4 + r) * WAVE + lane] = c01[r];
-            sh.G[(2 * 4 + r) * WAVE + lane] = c11[r];
-        }
-    }
-    __syncthreads();
-    if (wv == 0) {
-        if (NWM > 1 && R.nw > 1) {
-            double o[12];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                o[r] = sh.G[(0 * 4 + r) * WAVE + lane];
-                o[4 + r] = sh.G[(1 * 4 + r) * WAVE + lane];
-                o[8 + r] = sh.G[(2 * 4 + r) * WAVE + lane];
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) { c00[r] += o[r]; c01[r] += o[4 + r]; c11[r] += o[8 + r]; }
-        }
-        double vsum = 0.0;
-        if (lane < HM) {
-#pragma unroll
-            for (int q = 0; q < NWM; ++q)
-                if (q < R.nw) vsum += sh.red[R.buf][0][q * RW + lane];
-        }
-        __builtin_amdgcn_wave_barrier();
-        // lower triangle of G (row-major, this kernel's index type * HM + t: types a, v, budget)
-        auto kidx = [](int p) { const int t = p / 3, ty = p - 3 * t; return (ty == 0 ? 1 : (ty == 1 ? 0 : 2)) * HM + t; };
-#pragma unroll
-        for (int tile = 0; tile < 3; ++tile) {
-            const int I = tile == 2 ? 1 : 0, J = tile == 0 ? 0 : 1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = kk + 4 * r, col = i;
-                const int p = BW * I + row, q = BW * J + col;
-                const bool ok = row < BW && col < BW && p <= q && !(p == q && p % 3 == 0);
-                if (ok) {
-                    const int a = kidx(p), b = kidx(q);
-                    const double val = tile == 0 ? c00[r] : (tile == 1 ? c01[r] : c11[r]);
-                    sh.G[(a > b ? a : b) * KM + (a > b ? b : a)] = val;
-                }
-            }
-        }
-        if (lane < HM) sh.G[(HM + lane) * KM + HM + lane] = vsum;   // (v_t, v_t)
-    }
-    R.buf ^= Shared<HM, NWM>::NB - 1;
-}
-
 // Factor: slack reciprocals, per-asset LDL^T of Q, the Schur matrix G (one Q^{-1} column per
 // pass of a runtime loop), and its Cholesky factor (wave 0). Returns false on breakdown.
 //   G_jl = sum_i c_j c_l (Qi[tj][tl] - [vj] Qi[tj-1][tl] - [vl] Qi[tj][tl-1] + [vj vl] Qi[tj-1][tl-1])
@@ -1480,9 +1329,8 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM>& sh, Reducer<HM, N
     auto al = [&](int t) -> double { return t < H ? T.m[t] * sh.iden[t] * T.irsig : 0.0; };
     auto ep = [&](int t) -> double { return (t < H && T.ht) ? sh.sr[t] * T.bma(t) * T.P[t] : 0.0; };
     const int lane = glane<TH::GLN>(), wv = gwave<TH::GLN>();
-    if constexpr (mfma_gram<HM, NWM, TH>()) {
-        gram_mfma<HM, NWM>(T, sh, R, dq, Lr);
-    } else if constexpr (static_gram<HM, NWM>()) {
+    KMPC_PH(ph, 1);
+    if constexpr (static_gram<HM, NWM>()) {
         // Static-slot Gram: every entry (j, l) of G with period(j) <= period(l) = c has a
         // compile-time slot (gram_slot_jl). Each lane puts its contribution for slot s in
         // buf[s % 16]; a full chunk of 16 slots is reduce-scattered over the wave at once and the
@@ -1990,10 +1838,6 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                     const double smu = sg * mu;
                     double DL1[HM], DL2[HM], DL3[HM];
                     T.dual_dirs_all(DL1, DL2, DL3);
-                    constexpr int MP = pow2_at_least(HM);
-                    double pxp[MP];   // P (-rds + p2 + p3): the corrector's first px, reduced below
-#pragma unroll
-                    for (int t = 0; t < MP; ++t) pxp[t] = 0.0;
 #pragma unroll
                     for (int t = 0; t < HM; ++t) {
                         // the corrector's targets x l + dx_aff dl_aff - sigma mu (inactive lanes:
@@ -2006,21 +1850,12 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <=
                             r1 += T.dw[t] * dl1 - smu;
                             r2 += (T.ds[t] - dd) * dl2 - smu;
                             r3 += (T.ds[t] + dd) * dl3 - smu;
-                            if (KMPC_PX_CORR == 2 && T.hs && T.act) {
-                                double rdw, rds;
-                                dual_residual<HM, NWM>(T, sh, t, rdw, rds);
-                                pxp[t] = T.P[t] * (-rds - r2 * T.iz2[t] - r3 * T.iz3[t]);
-                            }
                         }
                         if (T.hw) T.rc1.set(t, r1);
                         if (T.hs) {
                             T.rc2.set(t, r2);
                             T.rc3.set(t, r3);
                         }
-                    }
-                    if (KMPC_PX_CORR == 2 && T.hs) {   // wave partials to sh.pxd, published by the barrier below
-                        const int slot = wave_reduce_scatter<MP, GL>(pxp);
-                        if ((glane<GL>() & ((GL / MP) - 1)) == 0) sh.pxd[gwave<GL>()][slot] = pxp[0];
                     }
                     if (gvt<GL>() < HM && T.ht && (int)gvt<GL>() < H) {
                         const int t = gvt<GL>();
