@@ -57,8 +57,8 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     return gelu_erf(x);
 }
 
-// Tile: 64 WT x 64 WT outputs per 256-thread block (4 waves, 2 x 2 of 32 WT x 32 WT), BK = 32.
-// WT = 2 (128 x 128) for large batches; WT = 1 (64 x 64) when 128-tiles would leave the 256 CUs
+// Tile: 64 WM x 64 WN outputs per 256-thread block (4 waves, 2 x 2 of 32 WM x 32 WN), BK = 32.
+// 128 x 128 for large batches; a smaller tile (KMPC_GEMM_MID) when 128-tiles would leave the 256 CUs
 // with fewer than two workgroups each (small window batches: configs[1]'s 4,096 windows).
 constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
 
@@ -87,16 +87,16 @@ __device__ __forceinline__ float epi_value(const GemmArgs& g, int m, int n, floa
     return v;
 }
 
-// fused epilogue of a WT x WT block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D
+// fused epilogue of a WM x WN block of 32 x 32 accumulator tiles (either MFMA dtype: the C/D
 // layout is dtype-independent on gfx950)
-template <int WT>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[WT][WT], int m0, int n0, int wm, int wn,
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, f32x16 (&acc)[WM][WN], int m0, int n0, int wm, int wn,
                                          int lane) {
     // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
-    for (int a = 0; a < WT; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < WT; ++b) {
+        for (int b = 0; b < WN; ++b) {
             const int n = n0 + wn + b * 32 + (lane & 31);
             if (n >= g.N) continue;
             const float bias = g.bias ? g.bias[n] : 0.0f;
@@ -137,21 +137,24 @@ __device__ __forceinline__ void xcd_tile(int& m0, int& n0, int tm = BM, int tn =
 #ifndef KMPC_GEMM_BK1
 #define KMPC_GEMM_BK1 32
 #endif
-template <int WT, int BKT = (WT == 1 ? KMPC_GEMM_BK1 : BK)>
+// Workgroup tile (64 WM) x (64 WN): 4 waves as 2 x 2, each a (32 WM) x (32 WN) block of 32 x 32
+// accumulator tiles. (1, 1) / (2, 2): the 64- / 128-square tiles; (2, 1): 128 x 64, half the
+// workgroups of the 64-square tile with each B fragment feeding two MFMAs.
+template <int WM, int WN, int BKT = ((WM == 1 && WN == 1) ? KMPC_GEMM_BK1 : BK)>
 __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
-    constexpr int TM = 64 * WT;
+    constexpr int TM = 64 * WM, TN = 64 * WN;
     constexpr int LS = BKT + 4;   // LDS row stride (floats): conflict-free ds_read_b128 fragments
     __shared__ float As[TM * LS];
-    __shared__ float Bs[TM * LS];
+    __shared__ float Bs[TN * LS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int m0, n0;
-    xcd_tile(m0, n0, TM, TM);
-    const int wm = (wv >> 1) * 32 * WT, wn = (wv & 1) * 32 * WT;
-    f32x16 acc[WT][WT];
+    xcd_tile(m0, n0, TM, TN);
+    const int wm = (wv >> 1) * 32 * WM, wn = (wv & 1) * 32 * WN;
+    f32x16 acc[WM][WN];
 #pragma unroll
-    for (int a = 0; a < WT; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < WT; ++b)
+        for (int b = 0; b < WN; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
@@ -164,78 +167,96 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
         kbeg = blockIdx.z * kc;
         kend = min(g.K, kbeg + kc);
     }
-    // A and B tiles: TM rows x BKT k = TM BKT / 4 float4 per operand, TM BKT / 1024 per thread. The
-    // next k-tile's global loads are issued into registers before this tile's MFMAs (register double
+    // A tile: TM rows x BKT k = TM BKT / 4 float4, TM BKT / 1024 per thread (B: TN rows). The next
+    // k-tile's global loads are issued into registers before this tile's MFMAs (register double
     // buffering: one LDS buffer, the HBM / L2 latency under the math).
-    constexpr int QN = TM * BKT / 1024;
+    constexpr int QA = TM * BKT / 1024, QB = TN * BKT / 1024;
     constexpr int RQ = BKT / 4;                     // float4 per row
-    f32x4 va[QN], vb[QN];
-    auto fetch = [&](int k0) {
+    f32x4 va[QA], vb[QB];
+    auto fetch_row = [&](const float* P, int ld, int rows, int r0, int row, int kk, f32x4& v) {
+        v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int rr = r0 + row;
+        if (rr >= rows) return;
+        if (vec_ok && kk + 3 < kend) {
+            v = *(const f32x4*)(P + (size_t)rr * ld + kk);
+        } else {
 #pragma unroll
-        for (int q = 0; q < QN; ++q) {
-            const int idx = tid + q * 256;          // 0 .. TM RQ - 1
-            const int row = idx / RQ, c4 = (idx % RQ) * 4;
-            const int kk = k0 + c4;
-            va[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-            vb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int ma = m0 + row, nb = n0 + row;
-            if (vec_ok && kk + 3 < kend) {
-                if (ma < g.M) va[q] = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
-                if (nb < g.N) vb[q] = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (kk + e < kend) {
-                        if (ma < g.M) va[q][e] = g.A[(size_t)ma * g.lda + kk + e];
-                        if (nb < g.N) vb[q][e] = g.B[(size_t)nb * g.ldb + kk + e];
-                    }
-                }
-            }
+            for (int e = 0; e < 4; ++e)
+                if (kk + e < kend) v[e] = P[(size_t)rr * ld + kk + e];
         }
     };
-    fetch(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+    auto fetch = [&](int k0) {
 #pragma unroll
-        for (int q = 0; q < QN; ++q) {
-            const int idx = tid + q * 256;
-            const int row = idx / RQ, c4 = (idx % RQ) * 4;
-            *(f32x4*)(As + row * LS + c4) = va[q];
-            *(f32x4*)(Bs + row * LS + c4) = vb[q];
+        for (int q = 0; q < QA; ++q) {
+            const int idx = tid + q * 256;          // 0 .. TM RQ - 1
+            fetch_row(g.A, g.lda, g.M, m0, idx / RQ, k0 + (idx % RQ) * 4, va[q]);
         }
-        __syncthreads();
-        if (k0 + BKT < kend) fetch(k0 + BKT);
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int idx = tid + q * 256;
+            fetch_row(g.B, g.ldb, g.N, n0, idx / RQ, k0 + (idx % RQ) * 4, vb[q]);
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int idx = tid + q * 256;
+            *(f32x4*)(As + (idx / RQ) * LS + (idx % RQ) * 4) = va[q];
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int idx = tid + q * 256;
+            *(f32x4*)(Bs + (idx / RQ) * LS + (idx % RQ) * 4) = vb[q];
+        }
+    };
+    auto compute = [&]() {
         const int r = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int kb = 0; kb < BKT; kb += 32) {   // 32-k sub-steps: lane (r, h) takes k = kb + 16 h + s
-            float af[WT][16], bf[WT][16];
+            float af[WM][16], bf[WN][16];
 #pragma unroll
-            for (int a = 0; a < WT; ++a) {
+            for (int a = 0; a < WM; ++a) {
                 const float* pa = As + (wm + a * 32 + r) * LS + kb + 16 * h;
-                const float* pb = Bs + (wn + a * 32 + r) * LS + kb + 16 * h;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const f32x4 x = *(const f32x4*)(pa + 4 * q);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) af[a][4 * q + e] = x[e];
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < WN; ++b) {
+                const float* pb = Bs + (wn + b * 32 + r) * LS + kb + 16 * h;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
                     const f32x4 y = *(const f32x4*)(pb + 4 * q);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) { af[a][4 * q + e] = x[e]; bf[a][4 * q + e] = y[e]; }
+                    for (int e = 0; e < 4; ++e) bf[b][4 * q + e] = y[e];
                 }
             }
 #pragma unroll
             for (int s = 0; s < 16; ++s)
 #pragma unroll
-                for (int a = 0; a < WT; ++a)
+                for (int a = 0; a < WM; ++a)
 #pragma unroll
-                    for (int b = 0; b < WT; ++b)
+                    for (int b = 0; b < WN; ++b)
                         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
         }
+    };
+    fetch(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+        stage();
+        __syncthreads();
+        if (k0 + BKT < kend) fetch(k0 + BKT);
+        compute();
         __syncthreads();
     }
     if (g.ksplit > 1) {   // raw partial of this K slice
         float* P = g.part + (size_t)blockIdx.z * g.M * g.N;
 #pragma unroll
-        for (int a = 0; a < WT; ++a)
+        for (int a = 0; a < WM; ++a)
 #pragma unroll
-            for (int b = 0; b < WT; ++b) {
+            for (int b = 0; b < WN; ++b) {
                 const int n = n0 + wn + b * 32 + (lane & 31);
                 if (n >= g.N) continue;
 #pragma unroll
@@ -246,7 +267,7 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
             }
         return;
     }
-    epilogue<WT>(g, acc, m0, n0, wm, wn, lane);
+    epilogue<WM, WN>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // split-K: C = epi(sum of the ksplit partials, in slice order)
@@ -326,7 +347,7 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
         }
         __syncthreads();
     }
-    epilogue<2>(g, acc, m0, n0, wm, wn, lane);
+    epilogue<2, 2>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
@@ -570,6 +591,11 @@ static bool latent_fusable(const kmpc_rollout_desc* d) {
 constexpr int SPLITK = 4;
 constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 
+// tile of the mid-size GEMMs (fewer than 512 128-square tiles): 11 = 64 x 64, 21 = 128 x 64,
+// 12 = 64 x 128, 22 = 128 x 128 (dev A/B: tools/ab_c2.sh)
+#ifndef KMPC_GEMM_MID
+#define KMPC_GEMM_MID 11
+#endif
 static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     g.ksplit = 1;
@@ -584,14 +610,21 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
         if (part && (size_t)grid64.x * grid64.y < 256 && g.K >= 128 * SPLITK) {
             g.ksplit = SPLITK;
             g.part = part;
-            hipLaunchKernelGGL(gemm_nt_kernel<1>, dim3(grid64.x, grid64.y, SPLITK), dim3(256), 0, s, g);
+            hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), dim3(grid64.x, grid64.y, SPLITK), dim3(256), 0, s, g);
             const size_t n = (size_t)g.M * g.N;
             hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
-        hipLaunchKernelGGL(gemm_nt_kernel<1>, grid64, dim3(256), 0, s, g);
+        if (KMPC_GEMM_MID == 21)
+            hipLaunchKernelGGL((gemm_nt_kernel<2, 1>), dim3((g.N + 63) / 64, (g.M + 127) / 128), dim3(256), 0, s, g);
+        else if (KMPC_GEMM_MID == 12)
+            hipLaunchKernelGGL((gemm_nt_kernel<1, 2>), dim3((g.N + 127) / 128, (g.M + 63) / 64), dim3(256), 0, s, g);
+        else if (KMPC_GEMM_MID == 22)
+            hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), grid64, dim3(256), 0, s, g);
     } else {
-        hipLaunchKernelGGL(gemm_nt_kernel<2>, grid, dim3(256), 0, s, g);
+        hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
     }
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }

@@ -43,13 +43,28 @@ __device__ __forceinline__ int wsumi(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
-constexpr int SIMPLEX_WAVES = 4;   // windows per 256-thread block
+constexpr int SIMPLEX_WAVES = 4;   // waves per 256-thread block
 constexpr int SIMPLEX_HR = 16;     // register fast path: N <= 64 assets, H <= 16 periods
 
-// N <= 64, H <= 16 (BASELINE configs[1]: N = 30, H = 5): lane i holds R_t,i of its asset for every
-// period in registers (one pass over yhat, one np_expf per element), and each wave reduction runs
-// over all periods at once (H independent butterflies interleaved, instead of H dependent rounds).
-// Same arithmetic and order as the general loop below: bit-identical results.
+// butterflies within aligned groups of G lanes (G = 32 or 64)
+template <int G>
+__device__ __forceinline__ float gmaxf(float v) {
+    for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+template <int G>
+__device__ __forceinline__ int gsumi(int v) {
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// N <= G (G = 32: two windows per wave; G = 64: one), H <= 16 (BASELINE configs[1]: N = 30, H = 5):
+// lane i of the window's lane group holds R_t,i of its asset for every period in registers (one
+// pass over yhat, one np_expf per element), and each group reduction runs over all periods at once
+// (H independent butterflies interleaved, instead of H dependent rounds). Same arithmetic and order
+// as the general loop below (a group butterfly over G lanes adds zeros where the wave-wide one did):
+// bit-identical results.
+template <int G>
 __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane) {
     constexpr int HR = SIMPLEX_HR;
     const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
@@ -68,7 +83,7 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
             bad |= !isfinite(R[t]);
         }
     }
-    if (wsumi(bad)) {
+    if (gsumi<G>(bad)) {
         if (act)
             for (int t = 0; t < tw; ++t) wout[(size_t)t * N + lane] = wpi;   // mpc.py:113-115
         if (lane == 0) {
@@ -82,7 +97,7 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
     int cnt[HR];
 #pragma unroll
     for (int t = 0; t < HR; ++t) rm[t] = R[t];
-    for (int o = 32; o > 0; o >>= 1)
+    for (int o = G / 2; o > 0; o >>= 1)
 #pragma unroll
         for (int t = 0; t < HR; ++t)
             if (t < H) rm[t] = fmaxf(rm[t], __shfl_xor(rm[t], o));
@@ -104,7 +119,7 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
     }
 #pragma unroll
     for (int t = 0; t < HR; ++t) cnt[t] = (t < H && act && R[t] == rm[t]) ? 1 : 0;
-    for (int o = 32; o > 0; o >>= 1)
+    for (int o = G / 2; o > 0; o >>= 1)
 #pragma unroll
         for (int t = 0; t < HR; ++t)
             if (t < H) cnt[t] += __shfl_xor(cnt[t], o);
@@ -122,7 +137,7 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
             wprev = wi;
         }
     }
-    for (int o = 32; o > 0; o >>= 1)
+    for (int o = G / 2; o > 0; o >>= 1)
 #pragma unroll
         for (int t = 0; t < HR; ++t)
             if (t < H) { rw[t] += __shfl_xor(rw[t], o); l1[t] += __shfl_xor(l1[t], o); }
@@ -139,10 +154,16 @@ __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane
 
 __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a) {
     const int lane = threadIdx.x & 63;
+    if (a.N <= 32 && a.H <= SIMPLEX_HR) {
+        // two windows per wave, one per 32-lane half
+        const int b = (blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+        if (b < a.B) simplex_regs<32>(a, b, lane & 31);   // (whole lane groups)
+        return;
+    }
     const int b = blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6);
     if (b >= a.B) return;   // (whole waves)
     if (a.N <= 64 && a.H <= SIMPLEX_HR) {
-        simplex_regs(a, b, lane);
+        simplex_regs<64>(a, b, lane);
         return;
     }
     const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
@@ -250,7 +271,8 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     a.trace = trace;
     if (a.B == 0) return KMPC_OK;
     if (simplex_case(a)) {
-        hipLaunchKernelGGL(simplex_kernel, dim3((a.B + SIMPLEX_WAVES - 1) / SIMPLEX_WAVES), dim3(64 * SIMPLEX_WAVES), 0,
+        const int per_block = SIMPLEX_WAVES * ((a.N <= 32 && a.H <= SIMPLEX_HR) ? 2 : 1);
+        hipLaunchKernelGGL(simplex_kernel, dim3((a.B + per_block - 1) / per_block), dim3(64 * SIMPLEX_WAVES), 0,
                            stream, a);
         return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
     }

@@ -11,7 +11,7 @@
 // per-window slab of the caller's workspace, [array][t][i] with the assets contiguous, so every
 // access is one coalesced wave load; each phase streams only the arrays it needs. The slack
 // reciprocals are recomputed from the state where they are used; the s-elimination coefficients
-// (P, bma P, bma) are written once per iteration by the factor pass and read by the Newton passes.
+// (P, bma P) are written once per iteration by the factor pass and read by the Newton passes.
 // The solve is bound by that HBM / Infinity-Cache stream.
 //
 // Layout: one workgroup per window, one asset per thread (blockDim = 64 ceil(N / 64) <= 1024), a
@@ -63,10 +63,11 @@ constexpr double LR_FLOOR = 1e-14;
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // per-(t, i) arrays of a window's slab (assets contiguous)
-// (P, BP = bma P and BMA are this iteration's s-elimination coefficients, written by the factor pass
-// so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state)
+// (P and BP = bma P are this iteration's s-elimination coefficients, written by the factor pass
+// so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state;
+// DS holds P bs, the s right-hand side already scaled by P)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
-             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, A_BMA, N_ARR };
+             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, N_ARR };
 
 __host__ __device__ inline size_t slab_doubles(int HM, int NP) {
     return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
@@ -240,10 +241,10 @@ struct Win {
         dl2 = hs() ? (-rc2 - e.l2 * (ds - dd)) * e.iz2 : 0.0;
         dl3 = hs() ? (-rc3 - e.l3 * (ds + dd)) * e.iz3 : 0.0;
     }
-    // ds of (t, i) from the stored DS (the back-substituted s right-hand sides summed over the
-    // direction's solves): ds = P (DS - rho pxa) — the s elimination's last step, never stored
-    __device__ __forceinline__ double dsv(int t, const St& e, double DSraw) const {
-        return hs() ? e.P * (DSraw - sh.rho[t] * sh.pxa[t]) : 0.0;
+    // ds of (t, i) from the stored DS (P times the back-substituted s right-hand sides, summed over
+    // the direction's solves): ds = DS - P rho pxa — the s elimination's last step, never stored
+    __device__ __forceinline__ double dsv(int t, const St& e, double DSp) const {
+        return hs() ? DSp - e.P * (sh.rho[t] * sh.pxa[t]) : 0.0;
     }
     __device__ __forceinline__ double alpha(int t, double m) const { return m * sh.iden[t] * irsig; }
     __device__ __forceinline__ double eps(int t, const St& e) const { return ht() ? sh.sr[t] * e.bma * e.P : 0.0; }
@@ -402,7 +403,6 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             P = cur.P;
             W.at(A_P, t) = cur.P;
             W.at(A_BP, t) = cur.bma * cur.P;
-            W.at(A_BMA, t) = cur.bma;
             // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
             const double Dd = pi + (nx ? En : 0.0);
             ok = ok && (Dd > 0.0) && (Dd < 1e300);
@@ -647,7 +647,33 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     // so Z^T x = Z^T x' + Gv c (Gv: the raw Gram's v-columns, kept by schur_factor) and
     // dw = x' - Q^-1 Z (q - E_v c). px is summed in the same block reduction as Z^T x'.
     const bool fused = W.fx != nullptr && ht;
-    if (fused) {
+    if (fused && !first) {
+        // refinement pass: the right-hand sides are the residual arrays (no targets), so the sweep
+        // needs no state — bs = R1 - lb5 / z4, rhs_w = R0 - BP bs_t + BP bs_{t+1}, px = sum_i P bs
+        double y = 0.0, bsc = 0.0, gpc = 0.0;
+        if (W.act) {
+            bsc = (double)W.at(A_R1, 0) - sh.lb5[0] * sh.iz4[0];
+            gpc = W.at(A_BP, 0) * bsc;
+        }
+        for (int t = 0; t < H; ++t) {
+            double pxv = 0.0;
+            if (W.act) {
+                double bsn = 0.0, gpn = 0.0;
+                if (t + 1 < H) {
+                    bsn = (double)W.at(A_R1, t + 1) - sh.lb5[t + 1] * sh.iz4[t + 1];
+                    gpn = W.at(A_BP, t + 1) * bsn;
+                }
+                y = ((double)W.at(A_R0, t) - gpc + gpn) + W.at(A_LR, t) * y;
+                W.at(A_Y, t) = y;
+                W.at(A_BS, t) = bsc;
+                pxv = W.at(A_P, t) * bsc;
+                bsc = bsn;
+                gpc = gpn;
+            }
+            pxv = wave_sum(pxv);   // (every lane of the wave: outside the divergent branch)
+            if ((threadIdx.x & (WAVE - 1)) == 0) W.pxr()[(threadIdx.x / WAVE) * HM + t] = pxv;
+        }
+    } else if (fused) {
         double y = 0.0;
         St cur{};
         double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0, r0c = 0.0, r1c = 0.0;
@@ -848,7 +874,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             schur_solve(sh, H);
         }
     }
-    // ---- C: dw = x - Q^{-1} (Z q) (DW), bs -= bma dd (BS), px = sum_i P bs ----
+    // ---- C: dw = x - Q^{-1} (Z q) (DW), P bs = P BS - BP dd (DS), px = sum_i P bs ----
     {
         if (W.act) {
             // Z q per period: alpha_t q_a + q_1 + eps_t q_v(t) - eps_{t+1} q_v(t+1); forward sweep (Y)
@@ -863,8 +889,8 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 epc = epn;
             }
         }
-        // backward sweep; dw_t = x_t - (Q^{-1} Z q)_t; at step t: bs_{t+1} -= bma_{t+1} (dw_{t+1} - dw_t)
-        double tn = 0.0, lrn = 0.0, dwn = 0.0, bman = 0.0, Pn = 0.0;
+        // backward sweep; dw_t = x_t - (Q^{-1} Z q)_t; at step t: P bs_{t+1} = P BS_{t+1} - BP_{t+1} (dw_{t+1} - dw_t)
+        double tn = 0.0, lrn = 0.0, dwn = 0.0, bpn = 0.0, Pn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double pxn = 0.0, px0 = 0.0;
             if (W.act) {
@@ -873,21 +899,21 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 lrn = W.at(A_LR, t);
                 const double dw = W.at(A_X, t) - tq;
                 if (first) W.at(A_DW, t) = dw; else W.at(A_DW, t) += dw;
-                const double bma = hs ? W.at(A_BMA, t) : 0.0, P = hs ? W.at(A_P, t) : 0.0;
-                // the back-substituted s right-hand side goes to DS (summed over the solves);
-                // ds = P (DS - rho pxa) is formed where it is read (Win::dsv)
+                const double bp = hs ? W.at(A_BP, t) : 0.0, P = hs ? W.at(A_P, t) : 0.0;
+                // P times the back-substituted s right-hand side goes to DS (summed over the
+                // solves); ds = DS - P rho pxa is formed where it is read (Win::dsv)
                 if (hs && t + 1 < H) {
-                    const double bs = W.at(A_BS, t + 1) - bman * (dwn - dw);
-                    if (first) W.at(A_DS, t + 1) = bs; else W.at(A_DS, t + 1) += bs;
-                    pxn = Pn * bs;
+                    const double pbs = Pn * W.at(A_BS, t + 1) - bpn * (dwn - dw);
+                    if (first) W.at(A_DS, t + 1) = pbs; else W.at(A_DS, t + 1) += pbs;
+                    pxn = pbs;
                 }
                 if (hs && t == 0) {
-                    const double bs = W.at(A_BS, 0) - bma * dw;
-                    if (first) W.at(A_DS, 0) = bs; else W.at(A_DS, 0) += bs;
-                    px0 = P * bs;
+                    const double pbs = P * W.at(A_BS, 0) - bp * dw;
+                    if (first) W.at(A_DS, 0) = pbs; else W.at(A_DS, 0) += pbs;
+                    px0 = pbs;
                 }
                 dwn = dw;
-                bman = bma;
+                bpn = bp;
                 Pn = P;
             }
             if (t + 1 < H) W.slot(t + 1, pxn);
