@@ -401,10 +401,10 @@ __device__ __forceinline__ int wave_reduce_scatter(double (&v)[M]) {
 // Per-thread [HM] arrays that are read less often than the state: in LDS ([t][thread], conflict
 // free) for blocks of <= 256 threads — the register file then holds the hot state without
 // spilling — and in registers for the 1024-thread variant (whose LDS could not hold them).
-template <int HM, int CS, bool LDS>
+template <int HM, int CS, bool LDS, int GL = 64>
 struct Cold;
-template <int HM, int CS>
-struct Cold<HM, CS, false> {
+template <int HM, int CS, int GL>
+struct Cold<HM, CS, false, GL> {
     double v[HM];
     __device__ __forceinline__ void bind(int) {}
     __device__ __forceinline__ double operator[](int t) const { return v[t]; }
@@ -415,11 +415,22 @@ extern __shared__ double kmpc_cold[];   // dynamic LDS: NC arrays of [HM][CS]
 // one base register + an immediate ds_read/ds_write offset. Lanes at or past CS share the slot of
 // lane CS - 1, an inactive asset: inactive lanes only ever store the same constants (zero
 // targets and reciprocals, unit pivots), so they read and write identical values there.
-template <int HM, int CS>
-struct Cold<HM, CS, true> {
+// Packed lane groups (GL < 64): each group of GL lanes owns CS / (64 / GL) consecutive slots, the
+// group's lanes past the last one sharing it (the same rule per window).
+template <int HM, int CS, int GL>
+struct Cold<HM, CS, true, GL> {
+    static constexpr int GS = GL < 64 ? CS / (64 / GL) : CS;   // slots per lane group
     int k;
     __device__ __forceinline__ void bind(int kk) { k = kk; }
-    __device__ __forceinline__ static int lane() { return (int)threadIdx.x < CS ? (int)threadIdx.x : CS - 1; }
+    __device__ __forceinline__ static int lane() {
+        const int tid = (int)threadIdx.x;
+        if constexpr (GL < 64) {
+            const int g = tid / GL, i = tid % GL;
+            return g * GS + (i < GS ? i : GS - 1);
+        } else {
+            return tid < CS ? tid : CS - 1;
+        }
+    }
     __device__ __forceinline__ double operator[](int t) const { return kmpc_cold[(k * HM + t) * CS + lane()]; }
     __device__ __forceinline__ void set(int t, double x) { kmpc_cold[(k * HM + t) * CS + lane()] = x; }
 };
@@ -506,10 +517,10 @@ struct Thread : Case<FL> {
     double w[HM], s[HM], l1[HM], l2[HM], l3[HM], m[HM];
     // per iteration: LDL^T of Q, P = 1/(alpha+beta); slack reciprocals (cold)
     double P[HM];
-    Cold<HM, CS, L && QL> iDd, Lr;   // (in registers unless QL)
-    Cold<HM, CS, L> iw, iz2, iz3;
+    Cold<HM, CS, L && QL, GL> iDd, Lr;   // (in registers unless QL)
+    Cold<HM, CS, L, GL> iw, iz2, iz3;
     // complementarity targets rc = z*l (- sigma mu + dz_aff dl_aff) (cold)
-    Cold<HM, CS, L> rc1, rc2, rc3;
+    Cold<HM, CS, L, GL> rc1, rc2, rc3;
     // direction
     double dw[HM], ds[HM];
 
@@ -1986,6 +1997,9 @@ int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
 
 namespace kmpc {
 
+#ifndef KMPC_PACK_NS   // cold-array slots per 16-lane window of the packed N <= 10 launch
+#define KMPC_PACK_NS 11
+#endif
 // Packed launcher: windows of N <= 32 assets (3 H <= GL) run 64 / GL per one-wave block, each on
 // its own lane group (GL = 16 for N <= 16 when 3 HM <= 16, else 32). Constant-case kernels for
 // H == HM in the two common cases (FL = 7, FL = 1), the generic kernel otherwise. Returns
@@ -1997,6 +2011,10 @@ int launch_ipm_packed(const SolveArgs& a, hipStream_t stream) {
     const bool exact = a.H == HM;
     if constexpr (3 * HM <= 16) {
         if (a.N <= 16) {
+            // N <= 10 (BASELINE configs[0]): the cold arrays at 11 slots per window instead of 16
+            // (44 per block): 29 -> 24 KB of LDS per block, six blocks per CU instead of five
+            if (exact && fl == 7 && a.N <= KMPC_PACK_NS - 1)
+                return launch_one<HM, 64, true, 7, 4 * KMPC_PACK_NS, false, 16>(a, 64, stream);
             if (exact && fl == 7) return launch_one<HM, 64, true, 7, 64, false, 16>(a, 64, stream);
             if (exact && fl == 1) return launch_one<HM, 64, true, 1, 64, false, 16>(a, 64, stream);
             return launch_one<HM, 64, false, -1, 64, false, 16>(a, 64, stream);
