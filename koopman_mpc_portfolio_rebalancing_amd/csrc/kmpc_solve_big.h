@@ -65,7 +65,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // per-(t, i) arrays of a window's slab (assets contiguous)
 // (P and BP = bma P are this iteration's s-elimination coefficients, written by the factor pass
 // so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state;
-// DS holds P bs, the s right-hand side already scaled by P)
+// DS holds P bs, the s right-hand side already scaled by P; RC* hold the corrector's targets
+// without the centring term -smu, which every reader subtracts)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
              A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, N_ARR };
 
@@ -150,6 +151,7 @@ struct Win {
     __device__ __forceinline__ double* gv() const { return fx; }
     __device__ __forceinline__ double* cv() const { return fx + KP * HM; }
     __device__ __forceinline__ double* pxr() const { return fx + KP * HM + HM; }
+
 
     __device__ __forceinline__ void bind(size_t slab_doubles) {
         rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, (int)(slab_doubles * sizeof(double)), 0x00020000);
@@ -299,28 +301,26 @@ struct Win {
         r2 = hs() ? (e.s - e.d) * e.l2 : 0.0;
         r3 = hs() ? (e.s + e.d) * e.l3 : 0.0;
     }
-    // corrector targets of (t, i) from the affine direction: x l + dx dl_aff - smu, written to RC*
-    // (ipm_kernel's corrector rows)
-    __device__ __forceinline__ void corr_rc(int t, const St& e, const Pre& p, double dd, double smu,
-                                            double& r1, double& r2, double& r3) const {
-        const double dw = p.dw, ds = dsv(t, e, p.ds);
+    // corrector targets of (t, i) from the affine direction: b = x l + dx dl_aff written to RC*,
+    // b - smu returned (ipm_kernel's corrector rows)
+    __device__ __forceinline__ void cbase(const St& e, double dw, double ds, double dd, double& b1, double& b2,
+                                          double& b3, double& dl1, double& dl2, double& dl3) const {
         double rc1, rc2, rc3;
         xl(e, rc1, rc2, rc3);
-        double dl1, dl2, dl3;
         ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
-        r1 = rc1;
-        r2 = rc2;
-        r3 = rc3;
-        if (hw()) {
-            r1 = rc1 + (dw * dl1 - smu);
-            at(A_RC1, t) = r1;
-        }
-        if (hs()) {
-            r2 = rc2 + ((ds - dd) * dl2 - smu);
-            r3 = rc3 + ((ds + dd) * dl3 - smu);
-            at(A_RC2, t) = r2;
-            at(A_RC3, t) = r3;
-        }
+        b1 = hw() ? rc1 + dw * dl1 : 0.0;
+        b2 = hs() ? rc2 + (ds - dd) * dl2 : 0.0;
+        b3 = hs() ? rc3 + (ds + dd) * dl3 : 0.0;
+    }
+    __device__ __forceinline__ void corr_rc(int t, const St& e, const Pre& p, double dd, double smu,
+                                            double& r1, double& r2, double& r3) const {
+        double b1, b2, b3, dl1, dl2, dl3;
+        cbase(e, p.dw, dsv(t, e, p.ds), dd, b1, b2, b3, dl1, dl2, dl3);
+        if (hw()) at(A_RC1, t) = b1;
+        if (hs()) { at(A_RC2, t) = b2; at(A_RC3, t) = b3; }
+        r1 = hw() ? b1 - smu : 0.0;
+        r2 = hs() ? b2 - smu : 0.0;
+        r3 = hs() ? b3 - smu : 0.0;
     }
 };
 
@@ -376,8 +376,10 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
     double W1c = 0.0, Ec = 0.0, pi = 0.0, lr = 0.0;
     double pm = 1.0;   // prod_{1<=k<=t} max(Lr_k, LR_FLOOR) = pm 2^pe (renormalised: no underflow)
     int pe = 0;
+    typename Win<HM, FL>::Pre pn{};   // the state of period t + 1, loaded at step t - 1
     if (W.act) {
         cur = W.st(0, W.wpi);
+        if (H > 1) pn = W.pre(1, false, false);
         W1c = cur.l1 * cur.iw;
         Ec = hs ? 4.0 * (cur.l2 * cur.iz2) * (cur.l3 * cur.iz3) * cur.P : 0.0;
         pi = W1c + Ec;
@@ -389,7 +391,8 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             St nxt = cur;
             double W1n = 0.0, En = 0.0;
             if (nx) {
-                nxt = W.st(t + 1, cur.w);
+                nxt = W.st(pn, cur.w);
+                if (t + 2 < H) pn = W.pre(t + 2, false, false);
                 W1n = nxt.l1 * nxt.iw;
                 En = hs ? 4.0 * (nxt.l2 * nxt.iz2) * (nxt.l3 * nxt.iz3) * nxt.P : 0.0;
             }
@@ -449,11 +452,13 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
 template <int HM, int FL>
 __device__ __forceinline__ void ph_record(Win<HM, FL>& W, double* wout, int tw) {
     auto& sh = W.sh;
-    double wprev = W.wpi;
+    double wprev = W.wpi, wn = 0.0;
+    if (W.act) wn = W.at(A_W, 0);
     for (int t = 0; t < W.H; ++t) {
         double v = 0.0;
         if (W.act) {
-            const double w = W.at(A_W, t);
+            const double w = wn;
+            if (t + 1 < W.H) wn = W.at(A_W, t + 1);
             if (t < tw) wout[t * W.N + W.i] = w;
             v = fabs(w - wprev);
             wprev = w;
@@ -478,15 +483,31 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
     // beta = dq pi. The v-type generators need period t-1's g / beta: period t's are written at
     // step t-1 (and period 0's after the loop), as is the direct (v_t, v_t) sum.
     {
-        double pi = W.act ? (double)W.at(A_X, 0) : 1.0;
+        struct Gv { double idd, lr, m, bp; };
+        auto ldG = [&](int t) {
+            Gv v;
+            v.idd = W.at(A_IDD, t);
+            v.lr = W.at(A_LR, t);
+            v.m = W.mload(t);
+            v.bp = W.ht() ? (double)W.at(A_BP, t) : 0.0;
+            return v;
+        };
+        Gv gnx{};
+        double pi = 1.0;
+        if (W.act) {
+            pi = W.at(A_X, 0);
+            gnx = ldG(H - 1);
+        }
         double dqn = 0.0, lrn = 0.0, gn = 0.0, bn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double vvn = 0.0;
             if (W.act) {
-                const double idd = W.at(A_IDD, t), lr = W.at(A_LR, t);
+                const Gv c = gnx;
+                if (t > 0) gnx = ldG(t - 1);
+                const double idd = c.idd, lr = c.lr;
                 const double dq = idd + lrn * lrn * dqn;
                 if (t + 1 < H) pi *= rcp(fmax(lrn, LR_FLOOR));
-                const double al = W.alpha(t, W.mload(t)), ep = W.epsa(t);
+                const double al = W.alpha(t, c.m), ep = W.ht() ? sh.sr[t] * c.bp : 0.0;
                 const double gt = rcp(pi), bt = dq * pi;
                 W.lg(3 * t + 1)[W.i] = al * gt;
                 W.lg(3 * t + 2)[W.i] = gt;
@@ -517,19 +538,11 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
     }
     W.finish(H);   // (its barriers also publish the generators to the workgroup)
     if ((int)threadIdx.x < H) sh.G[(3 * threadIdx.x) * LDG + 3 * threadIdx.x] = sh.tot[threadIdx.x];
-    // tiles (I, J), I <= J, of the 16-blocks in use, one wave per tile
-    const int NB = (K3 + 15) / 16, ntile = NB * (NB + 1) / 2;
-    for (int q = wv; q < ntile; q += W.nw) {
-        int I = 0, J = 0, rem = q;
-        for (int bi = 0; bi < NB; ++bi) {
-            const int n = NB - bi;
-            if (rem < n) { I = bi; J = bi + rem; break; }
-            rem -= n;
-        }
-        const double* pa = W.lg(16 * I + (lane & 15)) + (lane >> 4);
-        const double* pb = W.rg(16 * J + (lane & 15)) + (lane >> 4);
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int k0 = 0; k0 < N4; k0 += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k0], pb[k0], acc, 0, 0, 0);
+#ifndef KMPC_BIG_GRAM_SUPER
+#define KMPC_BIG_GRAM_SUPER 1
+#endif
+    const int NB = (K3 + 15) / 16;
+    auto store_tile = [&](int I, int J, const d4& acc) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int j = 16 * I + (lane >> 4) + 4 * r, l = 16 * J + (lane & 15);
@@ -538,6 +551,54 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
                 const bool use = tj < tl || (tj == tl && tyj <= tyl && !(tyj == 0 && tyl == 0));
                 if (use) sh.G[l * LDG + j] = acc[r];
             }
+        }
+    };
+    if (KMPC_BIG_GRAM_SUPER) {
+        // 32-row super-blocks: one wave per super tile (I2 <= J2) computes its 2 x 2 tiles (three on
+        // the diagonal) from two L and two R generator rows per k-step — each generator row is read
+        // by half as many waves as with one tile per wave (the generator stream is HBM traffic)
+        const int SB = (NB + 1) / 2, nst = SB * (SB + 1) / 2;
+        for (int q = wv; q < nst; q += W.nw) {
+            int I2 = 0, J2 = 0, rem = q;
+            for (int bi = 0; bi < SB; ++bi) {
+                const int n = SB - bi;
+                if (rem < n) { I2 = bi; J2 = bi + rem; break; }
+                rem -= n;
+            }
+            const bool i1 = 2 * I2 + 1 < NB, j1 = 2 * J2 + 1 < NB;   // second blocks in range
+            const bool t01 = j1, t10 = i1 && I2 != J2, t11 = i1 && j1;
+            const double* pa0 = W.lg(32 * I2 + (lane & 15)) + (lane >> 4);
+            const double* pa1 = W.lg(32 * I2 + 16 * i1 + (lane & 15)) + (lane >> 4);
+            const double* pb0 = W.rg(32 * J2 + (lane & 15)) + (lane >> 4);
+            const double* pb1 = W.rg(32 * J2 + 16 * j1 + (lane & 15)) + (lane >> 4);
+            d4 a00 = {0.0, 0.0, 0.0, 0.0}, a01 = a00, a10 = a00, a11 = a00;
+            for (int k0 = 0; k0 < N4; k0 += 4) {
+                const double x0 = pa0[k0], x1 = pa1[k0], y0 = pb0[k0], y1 = pb1[k0];
+                a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y0, a00, 0, 0, 0);
+                if (t01) a01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y1, a01, 0, 0, 0);
+                if (t10) a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y0, a10, 0, 0, 0);
+                if (t11) a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y1, a11, 0, 0, 0);
+            }
+            store_tile(2 * I2, 2 * J2, a00);
+            if (t01) store_tile(2 * I2, 2 * J2 + 1, a01);
+            if (t10) store_tile(2 * I2 + 1, 2 * J2, a10);
+            if (t11) store_tile(2 * I2 + 1, 2 * J2 + 1, a11);
+        }
+    } else {
+        // tiles (I, J), I <= J, of the 16-blocks in use, one wave per tile
+        const int ntile = NB * (NB + 1) / 2;
+        for (int q = wv; q < ntile; q += W.nw) {
+            int I = 0, J = 0, rem = q;
+            for (int bi = 0; bi < NB; ++bi) {
+                const int n = NB - bi;
+                if (rem < n) { I = bi; J = bi + rem; break; }
+                rem -= n;
+            }
+            const double* pa = W.lg(16 * I + (lane & 15)) + (lane >> 4);
+            const double* pb = W.rg(16 * J + (lane & 15)) + (lane >> 4);
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int k0 = 0; k0 < N4; k0 += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k0], pb[k0], acc, 0, 0, 0);
+            store_tile(I, J, acc);
         }
     }
     __syncthreads();
@@ -632,11 +693,9 @@ __device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H, const doub
 // the residual arrays R0 / R1, no targets), oracle/kmpc_oracle.c:lsolve. The solution is assigned
 // (first) or added to DW, DS and sh.dnu.
 // corr: the first solve of the corrector — its targets rc + dx_aff dl_aff - smu are formed here
-// from the affine direction (DW, DS) and written back to RC* (no sweep of their own). bn (when
-// non-null): this thread's ||b||_inf over the rows it owns (dual residual and rc targets).
+// from the affine direction (DW, DS) and written back to RC* without -smu (no sweep of their own).
 template <int HM, int FL>
-__device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr = false, double smu = 0.0,
-                                          double* bn = nullptr) {
+__device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr = false, double smu = 0.0) {
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
@@ -650,23 +709,37 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     if (fused && !first) {
         // refinement pass: the right-hand sides are the residual arrays (no targets), so the sweep
         // needs no state — bs = R1 - lb5 / z4, rhs_w = R0 - BP bs_t + BP bs_{t+1}, px = sum_i P bs
+        struct Rv { double r0, lr, P, r1n, bpn; };   // r1n / bpn: R1 / BP of period t + 1
+        auto ldR = [&](int t) {
+            Rv v;
+            v.r0 = W.at(A_R0, t);
+            v.lr = W.at(A_LR, t);
+            v.P = W.at(A_P, t);
+            v.r1n = t + 1 < H ? (double)W.at(A_R1, t + 1) : 0.0;
+            v.bpn = t + 1 < H ? (double)W.at(A_BP, t + 1) : 0.0;
+            return v;
+        };
+        Rv rn{};
         double y = 0.0, bsc = 0.0, gpc = 0.0;
         if (W.act) {
+            rn = ldR(0);
             bsc = (double)W.at(A_R1, 0) - sh.lb5[0] * sh.iz4[0];
             gpc = W.at(A_BP, 0) * bsc;
         }
         for (int t = 0; t < H; ++t) {
             double pxv = 0.0;
             if (W.act) {
+                const Rv c = rn;
+                if (t + 1 < H) rn = ldR(t + 1);
                 double bsn = 0.0, gpn = 0.0;
                 if (t + 1 < H) {
-                    bsn = (double)W.at(A_R1, t + 1) - sh.lb5[t + 1] * sh.iz4[t + 1];
-                    gpn = W.at(A_BP, t + 1) * bsn;
+                    bsn = c.r1n - sh.lb5[t + 1] * sh.iz4[t + 1];
+                    gpn = c.bpn * bsn;
                 }
-                y = ((double)W.at(A_R0, t) - gpc + gpn) + W.at(A_LR, t) * y;
+                y = (c.r0 - gpc + gpn) + c.lr * y;
                 W.at(A_Y, t) = y;
                 W.at(A_BS, t) = bsc;
-                pxv = W.at(A_P, t) * bsc;
+                pxv = c.P * bsc;
                 bsc = bsn;
                 gpc = gpn;
             }
@@ -674,28 +747,30 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             if ((threadIdx.x & (WAVE - 1)) == 0) W.pxr()[(threadIdx.x / WAVE) * HM + t] = pxv;
         }
     } else if (fused) {
+        // the first solve of a direction (refinement passes take the branch above)
         double y = 0.0;
         St cur{};
-        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0, r0c = 0.0, r1c = 0.0;
-        // bs of period t from its state, targets (first) or refinement residual
-        auto bsv = [&](int t, const St& e, double rc2, double rc3, double r1) -> double {
-            const double b1 = first ? -(W.cs_c - (e.l2 + e.l3 - sh.l4[t])) : r1;
-            const double p23 = first ? -rc2 * e.iz2 - rc3 * e.iz3 : 0.0;
+        double rc1c = 0.0, rc2c = 0.0, rc3c = 0.0, dwc = 0.0;
+        // bs of period t from its state and targets
+        auto bsv = [&](int t, const St& e, double rc2, double rc3) -> double {
+            const double b1 = -(W.cs_c - (e.l2 + e.l3 - sh.l4[t]));
+            const double p23 = -rc2 * e.iz2 - rc3 * e.iz3;
             return b1 + p23 - sh.lb5[t] * sh.iz4[t];
         };
-        double bsc = 0.0, gpc = 0.0;
+        typename Win<HM, FL>::Pre pq{};   // period t + 1's state (+ the affine direction), loaded at step t - 1
+        double bsc = 0.0, gpc = 0.0, lrc = 0.0;
         if (W.act) {
-            const auto p = W.pre(0, corr, false, !first);
+            const auto p = W.pre(0, corr, false);
+            if (H > 1) pq = W.pre(1, corr, false);
+            lrc = W.at(A_LR, 0);
             cur = W.st(p, W.wpi);
             if (corr) {
                 dwc = p.dw;
                 W.corr_rc(0, cur, p, dwc, smu, rc1c, rc2c, rc3c);
-            } else if (first) {
+            } else {
                 W.xl(cur, rc1c, rc2c, rc3c);
             }
-            r0c = p.r0;
-            r1c = p.r1;
-            bsc = bsv(0, cur, rc2c, rc3c, r1c);
+            bsc = bsv(0, cur, rc2c, rc3c);
             gpc = cur.bma * cur.P * bsc;
         }
         for (int t = 0; t < H; ++t) {
@@ -703,46 +778,39 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             if (W.act) {
                 const bool nx = t + 1 < H;
                 St nxt = cur;
-                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0, r0n = 0.0, r1n = 0.0;
+                double rc1n = 0.0, rc2n = 0.0, rc3n = 0.0, dwn = 0.0, lrn = 0.0;
                 if (nx) {
-                    const auto p = W.pre(t + 1, corr, false, !first);
+                    const auto p = pq;
+                    if (t + 2 < H) pq = W.pre(t + 2, corr, false);
+                    lrn = W.at(A_LR, t + 1);
                     nxt = W.st(p, cur.w);
                     if (corr) {
                         dwn = p.dw;
                         W.corr_rc(t + 1, nxt, p, dwn - dwc, smu, rc1n, rc2n, rc3n);
-                    } else if (first) {
+                    } else {
                         W.xl(nxt, rc1n, rc2n, rc3n);
                     }
-                    r0n = p.r0;
-                    r1n = p.r1;
                 }
-                double b0, p1 = 0.0, p2 = 0.0, p3 = 0.0, pn = 0.0;
-                if (first) {
-                    double rdw, rds;
-                    W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
-                    b0 = -rdw;
-                    p1 = hw ? -rc1c * cur.iw : 0.0;
-                    p2 = -rc2c * cur.iz2;
-                    p3 = -rc3c * cur.iz3;
-                    if (nx) pn = -rc3n * nxt.iz3 + rc2n * nxt.iz2;
-                    if (bn)
-                        *bn = fmax(*bn, fmax(fmax(fabs(rdw), fabs(rds)),
-                                             fmax(fabs(rc1c), fmax(fabs(rc2c), fabs(rc3c)))));
-                } else {
-                    b0 = r0c;
-                }
+                double rdw, rds;
+                W.dres(t, cur, nx ? nxt.l2 : 0.0, nx ? nxt.l3 : 0.0, rdw, rds);
+                const double b0 = -rdw;
+                const double p1 = hw ? -rc1c * cur.iw : 0.0;
+                const double p2 = -rc2c * cur.iz2;
+                const double p3 = -rc3c * cur.iz3;
+                const double pn = nx ? -rc3n * nxt.iz3 + rc2n * nxt.iz2 : 0.0;
                 const double bw = b0 + p1 + (p3 - p2) - pn;
-                const double bsn = nx ? bsv(t + 1, nxt, rc2n, rc3n, r1n) : 0.0;
+                const double bsn = nx ? bsv(t + 1, nxt, rc2n, rc3n) : 0.0;
                 const double gpn = nx ? nxt.bma * nxt.P * bsn : 0.0;
-                y = (bw - gpc + gpn) + W.at(A_LR, t) * y;   // forward sweep of Q^-1 (Y)
+                y = (bw - gpc + gpn) + lrc * y;   // forward sweep of Q^-1 (Y)
                 W.at(A_Y, t) = y;
                 W.at(A_BS, t) = bsc;
                 pxv = cur.P * bsc;
                 cur = nxt;
                 rc1c = rc1n; rc2c = rc2n; rc3c = rc3n;
-                dwc = dwn; r0c = r0n; r1c = r1n;
+                dwc = dwn;
                 bsc = bsn;
                 gpc = gpn;
+                lrc = lrn;
             }
             pxv = wave_sum(pxv);   // (every lane of the wave: outside the divergent branch)
             if ((threadIdx.x & (WAVE - 1)) == 0) W.pxr()[(threadIdx.x / WAVE) * HM + t] = pxv;
@@ -796,9 +864,6 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                         p3 = -rc3c * cur.iz3;
                         if (nx) pn = -rc3n * nxt.iz3 + rc2n * nxt.iz2;
                     }
-                    if (bn)
-                        *bn = fmax(*bn, fmax(fmax(fabs(rdw), fabs(rds)),
-                                             fmax(fabs(rc1c), fmax(fabs(rc2c), fabs(rc3c)))));
                 } else {
                     b0 = r0c;
                     b1 = r1c;
@@ -838,17 +903,33 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             }
         }
         // backward sweep x_t = y_t / Dd_t + Lr_{t+1} x_{t+1} (X), with the Z^T x slots: at step t,
-        // v-slot t+1 = eps_{t+1} (x_{t+1} - x_t), a-slot t = alpha_t x_t, 1-slot t = x_t
+        // v-slot t+1 = eps_{t+1} (x_{t+1} - x_t), a-slot t = alpha_t x_t, 1-slot t = x_t.
+        // Every sweep below loads period t -+ 1 before it computes period t (two periods of loads
+        // in flight per wave: the slab stream is bound by loads in flight, not by the arithmetic).
+        struct Bv { double y, idd, bp, m, lr; };
+        auto ldB = [&](int t) {
+            Bv v;
+            v.y = W.at(A_Y, t);
+            v.idd = W.at(A_IDD, t);
+            v.bp = ht ? (double)W.at(A_BP, t) : 0.0;
+            v.m = W.mload(t);
+            v.lr = W.at(A_LR, t);
+            return v;
+        };
+        Bv bn{};
+        if (W.act) bn = ldB(H - 1);
         double xn = 0.0, lrn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double x = 0.0, va = 0.0, vv1 = 0.0, ep = 0.0;
             if (W.act) {
-                x = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * xn;
+                const Bv c = bn;
+                if (t > 0) bn = ldB(t - 1);
+                x = c.y * c.idd + lrn * xn;
                 W.at(A_X, t) = x;
-                ep = W.epsa(t);
-                va = W.alpha(t, W.mload(t)) * x;
+                ep = ht ? sh.sr[t] * c.bp : 0.0;
+                va = W.alpha(t, c.m) * x;
                 vv1 = (t + 1 < H) ? epn * (xn - x) : 0.0;
-                lrn = W.at(A_LR, t);
+                lrn = c.lr;
             }
             if (t + 1 < H) W.slot(t + 1, vv1);
             W.slot(H + t, va);
@@ -878,43 +959,72 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
     {
         if (W.act) {
             // Z q per period: alpha_t q_a + q_1 + eps_t q_v(t) - eps_{t+1} q_v(t+1); forward sweep (Y)
+            struct Fv { double m, bpn, lr; };   // bpn: BP of period t + 1
+            auto ldF = [&](int t) {
+                Fv v;
+                v.m = W.mload(t);
+                v.bpn = (ht && t + 1 < H) ? (double)W.at(A_BP, t + 1) : 0.0;
+                v.lr = W.at(A_LR, t);
+                return v;
+            };
+            Fv fn = ldF(0);
             double y = 0.0;
             double epc = W.epsa(0);
             for (int t = 0; t < H; ++t) {
-                const double epn = (t + 1 < H) ? W.epsa(t + 1) : 0.0;
-                const double zq = W.alpha(t, W.mload(t)) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
+                const Fv c = fn;
+                if (t + 1 < H) fn = ldF(t + 1);
+                const double epn = (t + 1 < H) ? sh.sr[t + 1] * c.bpn : 0.0;
+                const double zq = W.alpha(t, c.m) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
                                   ((t + 1 < H) ? epn * sh.q[3 * t + 3] : 0.0);
-                y = zq + W.at(A_LR, t) * y;
+                y = zq + c.lr * y;
                 W.at(A_Y, t) = y;
                 epc = epn;
             }
         }
         // backward sweep; dw_t = x_t - (Q^{-1} Z q)_t; at step t: P bs_{t+1} = P BS_{t+1} - BP_{t+1} (dw_{t+1} - dw_t)
+        // (refinement passes add to DW / DS: their old values are loaded with the period)
+        struct Cv { double y, idd, lr, x, bp, P, bs1, dwo, ds1; };   // bs1 / ds1: BS / DS of period t + 1
+        auto ldC = [&](int t) {
+            Cv v;
+            v.y = W.at(A_Y, t);
+            v.idd = W.at(A_IDD, t);
+            v.lr = W.at(A_LR, t);
+            v.x = W.at(A_X, t);
+            v.bp = hs ? (double)W.at(A_BP, t) : 0.0;
+            v.P = hs ? (double)W.at(A_P, t) : 0.0;
+            v.bs1 = (hs && t + 1 < H) ? (double)W.at(A_BS, t + 1) : 0.0;
+            v.dwo = first ? 0.0 : (double)W.at(A_DW, t);
+            v.ds1 = (!first && hs && t + 1 < H) ? (double)W.at(A_DS, t + 1) : 0.0;
+            return v;
+        };
+        Cv cn{};
+        if (W.act) cn = ldC(H - 1);
         double tn = 0.0, lrn = 0.0, dwn = 0.0, bpn = 0.0, Pn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double pxn = 0.0, px0 = 0.0;
             if (W.act) {
-                const double tq = W.at(A_Y, t) * W.at(A_IDD, t) + lrn * tn;
+                const Cv c = cn;
+                if (t > 0) cn = ldC(t - 1);
+                const double tq = c.y * c.idd + lrn * tn;
                 tn = tq;
-                lrn = W.at(A_LR, t);
-                const double dw = W.at(A_X, t) - tq;
-                if (first) W.at(A_DW, t) = dw; else W.at(A_DW, t) += dw;
-                const double bp = hs ? W.at(A_BP, t) : 0.0, P = hs ? W.at(A_P, t) : 0.0;
+                lrn = c.lr;
+                const double dw = c.x - tq;
+                W.at(A_DW, t) = first ? dw : c.dwo + dw;
                 // P times the back-substituted s right-hand side goes to DS (summed over the
                 // solves); ds = DS - P rho pxa is formed where it is read (Win::dsv)
                 if (hs && t + 1 < H) {
-                    const double pbs = Pn * W.at(A_BS, t + 1) - bpn * (dwn - dw);
-                    if (first) W.at(A_DS, t + 1) = pbs; else W.at(A_DS, t + 1) += pbs;
+                    const double pbs = Pn * c.bs1 - bpn * (dwn - dw);
+                    W.at(A_DS, t + 1) = first ? pbs : c.ds1 + pbs;
                     pxn = pbs;
                 }
                 if (hs && t == 0) {
-                    const double pbs = P * W.at(A_BS, 0) - bp * dw;
+                    const double pbs = c.P * W.at(A_BS, 0) - c.bp * dw;
                     if (first) W.at(A_DS, 0) = pbs; else W.at(A_DS, 0) += pbs;
                     px0 = pbs;
                 }
                 dwn = dw;
-                bpn = bp;
-                Pn = P;
+                bpn = c.bp;
+                Pn = c.P;
             }
             if (t + 1 < H) W.slot(t + 1, pxn);
             if (t == 0) W.slot(0, px0);
@@ -952,13 +1062,13 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
         sh.lb6[t] = sh.b6[t];
     }
     __syncthreads();
-    // ||b||_inf of the unreduced system: this thread's rows from the first solve's sweep, the
-    // owner rows here; reduced with the first residual norm
+    // ||b||_inf of the unreduced system: this thread's rows in the first residual pass, the owner
+    // rows here; reduced with the first residual norm
     double bn = 0.0;
     if (n_refine > 0 && threadIdx.x == 0)
         for (int t = 0; t < H; ++t) bn = fmax(bn, fmax(fabs(sh.b5[t]), fabs(sh.b6[t])));
     for (int r = 0;; ++r) {
-        ph_lsolve(W, r == 0, corr && r == 0, smu, n_refine > 0 && r == 0 ? &bn : nullptr);
+        ph_lsolve(W, r == 0, corr && r == 0, smu);
         if (r >= n_refine) break;
         // residual of rows (1), (2), (7) of the direction; rows (3)-(6) hold by construction
         for (int t = 0; t < H; ++t) {
@@ -986,10 +1096,21 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
                 const St e = W.st(t, W.wprev(t));
                 const double dw = W.at(A_DW, t), ds = W.dsv(t, e, W.at(A_DS, t));
                 const double dd = dw - (t ? W.at(A_DW, t - 1) : 0.0);
+                // the targets: the corrector's (stored without -smu), or the predictor's x l
+                double rc1, rc2, rc3;
+                if (corr) {
+                    rc1 = W.hw() ? W.at(A_RC1, t) - smu : 0.0;
+                    rc2 = hs ? W.at(A_RC2, t) - smu : 0.0;
+                    rc3 = hs ? W.at(A_RC3, t) - smu : 0.0;
+                } else {
+                    W.xl(e, rc1, rc2, rc3);
+                }
                 double dl1, dl2, dl3;
-                W.ddirs(e, W.at(A_RC1, t), W.at(A_RC2, t), W.at(A_RC3, t), dw, ds, dd, dl1, dl2, dl3);
+                W.ddirs(e, rc1, rc2, rc3, dw, ds, dd, dl1, dl2, dl3);
                 double rdw, rds;
                 W.dres(t, e, l2n, l3n, rdw, rds);
+                if (r == 0)
+                    bn = fmax(bn, fmax(fmax(fabs(rdw), fabs(rds)), fmax(fabs(rc1), fmax(fabs(rc2), fabs(rc3)))));
                 const double dl4 = ht ? (sh.b5[t] + sh.l4[t] * sh.sds[t]) * sh.iz4[t] : 0.0;
                 const double r0 = -rdw - (W.alpha(t, e.m) * sh.adw[t] - (dl1 + (dl3 - dl2) - (nl3 - nl2)) + sh.dnu[t]);
                 const double r1 = hs ? -rds + (dl2 + dl3 - dl4) : 0.0;
@@ -1030,7 +1151,7 @@ __device__ __forceinline__ void ph_newton(Win<HM, FL>& W, int n_refine, bool cor
 // max_step does the same).
 // pred: the predictor's direction, whose targets are x l (from the state, not stored)
 template <int HM, int FL>
-__device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2, bool pred) {
+__device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2, bool pred, double smu = 0.0) {
     auto& sh = W.sh;
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
     const int H = W.H;
@@ -1047,7 +1168,7 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
             wprev = e.w;
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
-            double r1 = p.rc1, r2 = p.rc2, r3 = p.rc3;
+            double r1 = p.rc1 - smu, r2 = p.rc2 - smu, r3 = p.rc3 - smu;   // (RC* without -smu)
             if (pred) W.xl(e, r1, r2, r3);
             double dl1, dl2, dl3;
             W.ddirs(e, r1, r2, r3, dw, ds, dd, dl1, dl2, dl3);
@@ -1089,7 +1210,7 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
 // iterate update (the multiplier directions need the old state: w_{t-1} is carried), fused with
 // the next iteration's period sums (ph_sums) over the updated w, s
 template <int HM, int FL>
-__device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
+__device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double smu) {
     auto& sh = W.sh;
     const int H = W.H;
     double wprev = W.wpi, dwp = 0.0;
@@ -1105,7 +1226,7 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step) {
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
-            W.ddirs(e, p.rc1, p.rc2, p.rc3, dw, ds, dd, dl1, dl2, dl3);
+            W.ddirs(e, p.rc1 - smu, p.rc2 - smu, p.rc3 - smu, dw, ds, dd, dl1, dl2, dl3);   // (RC* without -smu)
             W.at(A_L1, t) = e.l1 + step * dl1;
             W.at(A_L2, t) = e.l2 + step * dl2;
             W.at(A_L3, t) = e.l3 + step * dl3;
@@ -1169,7 +1290,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         for (int pass = 0; pass < 2; ++pass) {
             ph_newton(W, (pass == 0 || mu > (W.hw() ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : a.n_refine, pass == 1, smu);
             double cc1, cc2;
-            const double amax = ph_step(W, cc1, cc2, pass == 0);
+            const double amax = ph_step(W, cc1, cc2, pass == 0, smu);
             if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
             const double ap = fmin(1.0, amax);
             double comp = mu_l + ap * (cc1 + ap * cc2);
@@ -1180,7 +1301,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
             smu = sg * mu;   // the corrector's targets are formed inside its first solve
         }
         if (a.trace && b == 0 && threadIdx.x == 0) a.trace[4 * it + 3] = step;
-        ph_update(W, step);
+        ph_update(W, step, smu);
     }
     return it;
 }
