@@ -1157,13 +1157,24 @@ __device__ __forceinline__ double ph_step(Win<HM, FL>& W, double& c1, double& c2
     const int H = W.H;
     double a = 1e300, wprev = W.wpi, dwp = 0.0;
     c1 = c2 = 0.0;
-    typename Win<HM, FL>::Pre pn{};
-    if (W.act) pn = W.pre(0, true, !pred);
+#ifndef KMPC_BIG_PF2   // step length and update sweeps: loads two periods ahead (1) or one (0)
+#define KMPC_BIG_PF2 1
+#endif
+    typename Win<HM, FL>::Pre pn{}, pn2{};
+    if (W.act) {
+        pn = W.pre(0, true, !pred);
+        if (KMPC_BIG_PF2 && H > 1) pn2 = W.pre(1, true, !pred);
+    }
     for (int t = 0; t < H; ++t) {
         double mdw = 0.0;
         if (W.act) {
             const auto p = pn;
-            if (t + 1 < H) pn = W.pre(t + 1, true, !pred);
+            if (KMPC_BIG_PF2) {
+                pn = pn2;
+                if (t + 2 < H) pn2 = W.pre(t + 2, true, !pred);
+            } else if (t + 1 < H) {
+                pn = W.pre(t + 1, true, !pred);
+            }
             const St e = W.st(p, wprev);
             wprev = e.w;
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
@@ -1214,13 +1225,21 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
     auto& sh = W.sh;
     const int H = W.H;
     double wprev = W.wpi, dwp = 0.0;
-    typename Win<HM, FL>::Pre pn{};
-    if (W.act) pn = W.pre(0);
+    typename Win<HM, FL>::Pre pn{}, pn2{};
+    if (W.act) {
+        pn = W.pre(0);
+        if (KMPC_BIG_PF2 && H > 1) pn2 = W.pre(1);
+    }
     for (int t = 0; t < H; ++t) {
         double mw = 0.0, wn = 0.0, sn = 0.0;
         if (W.act) {
             const auto p = pn;
-            if (t + 1 < H) pn = W.pre(t + 1);
+            if (KMPC_BIG_PF2) {
+                pn = pn2;
+                if (t + 2 < H) pn2 = W.pre(t + 2);
+            } else if (t + 1 < H) {
+                pn = W.pre(t + 1);
+            }
             const St e = W.st(p, wprev);
             wprev = e.w;
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
