@@ -44,7 +44,7 @@ HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 # per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
-PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03_solve_pmc.json")
+PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04_solve_pmc.json")
 
 
 def solve_flop_model(N: int, H: int) -> dict:
@@ -253,8 +253,9 @@ def cpu_baseline(sd, mean, std, x_gpu, wp_gpu, W0_gpu, val_gpu, y_gpu, H, N, cfg
         return time.perf_counter() - t0, y, W, st
 
     try:
-        dt, _, _, _ = run(0, 2 * cores)                    # calibration (+ warms BLAS / OpenMP)
-        per = dt / (2 * cores)
+        run(0, 2 * cores)                                  # warms BLAS / OpenMP
+        dt, _, _, _ = run(0, 8 * cores)                    # calibration
+        per = dt / (8 * cores)
         n = int(min(max(budget_s / max(per, 1e-6), 2 * cores), x_gpu.shape[0]))
         dt, y, W, st = run(0, n)
     finally:
