@@ -57,9 +57,9 @@ __device__ __forceinline__ float apply_act(float x, int act) {
     return gelu_erf(x);
 }
 
-// Tile: 64 WM x 64 WN outputs per 256-thread block (4 waves, 2 x 2 of 32 WM x 32 WN), BK = 32.
-// 128 x 128 for large batches; a smaller tile (KMPC_GEMM_MID) when 128-tiles would leave the 256 CUs
-// with fewer than two workgroups each (small window batches: configs[1]'s 4,096 windows).
+// Tile: GM x GN waves per block, each a (32 WM) x (32 WN) block of 32 x 32 accumulator tiles, BK = 32.
+// 128 x 128 as 4 x 2 waves of 32 x 64 (512 threads) for every GEMM with at least 256 such tiles;
+// split K for the narrow last encoder layer of small batches (configs[1]).
 constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
 
 // C = epi(A . B^T). Each lane of an MFMA consumes 16 contiguous k (k = 16h + s, h = lane >> 5),
@@ -140,16 +140,19 @@ __device__ __forceinline__ void xcd_tile(int& m0, int& n0, int tm = BM, int tn =
 // Workgroup tile (64 WM) x (64 WN): 4 waves as 2 x 2, each a (32 WM) x (32 WN) block of 32 x 32
 // accumulator tiles. (1, 1) / (2, 2): the 64- / 128-square tiles; (2, 1): 128 x 64, half the
 // workgroups of the 64-square tile with each B fragment feeding two MFMAs.
-template <int WM, int WN, int BKT = ((WM == 1 && WN == 1) ? KMPC_GEMM_BK1 : BK)>
-__global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
-    constexpr int TM = 64 * WM, TN = 64 * WN;
+// GM x GN waves per workgroup (2 x 2: 256 threads; 4 x 2: 512 threads, two waves per SIMD for the
+// one-workgroup-per-CU grids)
+template <int WM, int WN, int BKT = ((WM == 1 && WN == 1) ? KMPC_GEMM_BK1 : BK), int GM = 2, int GN = 2>
+__global__ void __launch_bounds__(64 * GM * GN) gemm_nt_kernel(GemmArgs g) {
+    constexpr int NT = 64 * GM * GN;
+    constexpr int TM = 32 * GM * WM, TN = 32 * GN * WN;
     constexpr int LS = BKT + 4;   // LDS row stride (floats): conflict-free ds_read_b128 fragments
     __shared__ float As[TM * LS];
     __shared__ float Bs[TN * LS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int m0, n0;
     xcd_tile(m0, n0, TM, TN);
-    const int wm = (wv >> 1) * 32 * WM, wn = (wv & 1) * 32 * WN;
+    const int wm = (wv / GN) * 32 * WM, wn = (wv % GN) * 32 * WN;
     f32x16 acc[WM][WN];
 #pragma unroll
     for (int a = 0; a < WM; ++a)
@@ -170,7 +173,8 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     // A tile: TM rows x BKT k = TM BKT / 4 float4, TM BKT / 1024 per thread (B: TN rows). The next
     // k-tile's global loads are issued into registers before this tile's MFMAs (register double
     // buffering: one LDS buffer, the HBM / L2 latency under the math).
-    constexpr int QA = TM * BKT / 1024, QB = TN * BKT / 1024;
+    constexpr int QA = TM * BKT / (4 * NT), QB = TN * BKT / (4 * NT);
+    static_assert(QA * 4 * NT == TM * BKT && QB * 4 * NT == TN * BKT, "tile loads per thread");
     constexpr int RQ = BKT / 4;                     // float4 per row
     f32x4 va[QA], vb[QB];
     auto fetch_row = [&](const float* P, int ld, int rows, int r0, int row, int kk, f32x4& v) {
@@ -188,24 +192,24 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs g) {
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
-            const int idx = tid + q * 256;          // 0 .. TM RQ - 1
+            const int idx = tid + q * NT;           // 0 .. TM RQ - 1
             fetch_row(g.A, g.lda, g.M, m0, idx / RQ, k0 + (idx % RQ) * 4, va[q]);
         }
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
-            const int idx = tid + q * 256;
+            const int idx = tid + q * NT;
             fetch_row(g.B, g.ldb, g.N, n0, idx / RQ, k0 + (idx % RQ) * 4, vb[q]);
         }
     };
     auto stage = [&]() {
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
-            const int idx = tid + q * 256;
+            const int idx = tid + q * NT;
             *(f32x4*)(As + (idx / RQ) * LS + (idx % RQ) * 4) = va[q];
         }
 #pragma unroll
         for (int q = 0; q < QB; ++q) {
-            const int idx = tid + q * 256;
+            const int idx = tid + q * NT;
             *(f32x4*)(Bs + (idx / RQ) * LS + (idx % RQ) * 4) = vb[q];
         }
     };
@@ -592,9 +596,14 @@ constexpr int SPLITK = 4;
 constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 
 // tile of the mid-size GEMMs (fewer than 512 128-square tiles): 11 = 64 x 64, 21 = 128 x 64,
-// 12 = 64 x 128, 22 = 128 x 128 (dev A/B: tools/ab_c2.sh)
+// 12 = 64 x 128, 22 = 128 x 128 (4 waves), 42 = 128 x 128 as 4 x 2 waves of 32 x 64 (512 threads:
+// two waves per SIMD at one workgroup per CU) — measured best at both sizes (dev A/B:
+// tools/ab_c2.sh)
 #ifndef KMPC_GEMM_MID
-#define KMPC_GEMM_MID 11
+#define KMPC_GEMM_MID 42
+#endif
+#ifndef KMPC_GEMM_BIG   // tile of the large GEMMs: 22 = 128 x 128 (4 waves), 42 (8 waves), 82 = 256 x 128 (16 waves)
+#define KMPC_GEMM_BIG 42
 #endif
 static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
@@ -621,8 +630,14 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
             hipLaunchKernelGGL((gemm_nt_kernel<1, 2>), dim3((g.N + 127) / 128, (g.M + 63) / 64), dim3(256), 0, s, g);
         else if (KMPC_GEMM_MID == 22)
             hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
+        else if (KMPC_GEMM_MID == 42)   // 128 x 128, 8 waves of 32 x 64
+            hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
         else
             hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), grid64, dim3(256), 0, s, g);
+    } else if (KMPC_GEMM_BIG == 42) {   // 128 x 128, 8 waves of 32 x 64
+        hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
+    } else if (KMPC_GEMM_BIG == 82) {   // 256 x 128, 16 waves of 32 x 64
+        hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 8, 2>), dim3((g.N + 127) / 128, (g.M + 255) / 256), dim3(1024), 0, s, g);
     } else {
         hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
     }
