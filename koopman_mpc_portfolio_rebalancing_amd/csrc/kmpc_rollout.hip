@@ -58,8 +58,9 @@ __device__ __forceinline__ float apply_act(float x, int act) {
 }
 
 // Tile: GM x GN waves per block, each a (32 WM) x (32 WN) block of 32 x 32 accumulator tiles, BK = 32.
-// 128 x 128 as 4 x 2 waves of 32 x 64 (512 threads) for every GEMM with at least 256 such tiles;
-// split K for the narrow last encoder layer of small batches (configs[1]).
+// 128 x 128 as 4 x 2 waves of 32 x 64 (512 threads) for GEMMs with 512 or more such tiles, as 4 x 4
+// waves of 32 x 32 (1024 threads) below that (one workgroup per CU); split K for the narrow last
+// encoder layer of small batches (configs[1]).
 constexpr int BM = 128, BN = 128, BK = 32, LDS_STRIDE = BK + 4;
 
 // C = epi(A . B^T). Each lane of an MFMA consumes 16 contiguous k (k = 16h + s, h = lane >> 5),
@@ -597,10 +598,11 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 
 // tile of the mid-size GEMMs (fewer than 512 128-square tiles): 11 = 64 x 64, 21 = 128 x 64,
 // 12 = 64 x 128, 22 = 128 x 128 (4 waves), 42 = 128 x 128 as 4 x 2 waves of 32 x 64 (512 threads:
-// two waves per SIMD at one workgroup per CU) — measured best at both sizes (dev A/B:
+// two waves per SIMD at one workgroup per CU), 44 = 128 x 128 as 4 x 4 waves of 32 x 32 (1024
+// threads, four per SIMD) — 44 measured best here, 42 for the large GEMMs (dev A/B:
 // tools/ab_c2.sh)
 #ifndef KMPC_GEMM_MID
-#define KMPC_GEMM_MID 42
+#define KMPC_GEMM_MID 44
 #endif
 #ifndef KMPC_GEMM_BIG   // tile of the large GEMMs: 22 = 128 x 128 (4 waves), 42 (8 waves), 82 = 256 x 128 (16 waves)
 #define KMPC_GEMM_BIG 42
@@ -632,10 +634,14 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
             hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
         else if (KMPC_GEMM_MID == 42)   // 128 x 128, 8 waves of 32 x 64
             hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
+        else if (KMPC_GEMM_MID == 44)   // 128 x 128, 16 waves of 32 x 32
+            hipLaunchKernelGGL((gemm_nt_kernel<1, 1, BK, 4, 4>), grid, dim3(1024), 0, s, g);
         else
             hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), grid64, dim3(256), 0, s, g);
     } else if (KMPC_GEMM_BIG == 42) {   // 128 x 128, 8 waves of 32 x 64
         hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
+    } else if (KMPC_GEMM_BIG == 44) {   // 128 x 128, 16 waves of 32 x 32
+        hipLaunchKernelGGL((gemm_nt_kernel<1, 1, BK, 4, 4>), grid, dim3(1024), 0, s, g);
     } else if (KMPC_GEMM_BIG == 82) {   // 256 x 128, 16 waves of 32 x 64
         hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 8, 2>), dim3((g.N + 127) / 128, (g.M + 255) / 256), dim3(1024), 0, s, g);
     } else {
