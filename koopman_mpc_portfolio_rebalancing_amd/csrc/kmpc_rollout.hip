@@ -451,22 +451,26 @@ __device__ __forceinline__ void tile_dot(const float* As, int lda, const float* 
     for (int i = 0; i < 16; ++i) acc[i] += acc1[i];
 }
 
-__global__ void __launch_bounds__(256) latent_steps_kernel(LatentArgs a) {
+#ifndef KMPC_LAT_WAVES   // waves per block of latent_steps_kernel
+#define KMPC_LAT_WAVES 4
+#endif
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV) latent_steps_kernel(LatentArgs a) {
     extern __shared__ float zs[];   // [2][32][L + 4]
     const int L = a.L, LS = L + 4, N = a.N;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
     const int m0 = blockIdx.x * LAT_ROWS;
     float* zc = zs;
     float* zn = zs + LAT_ROWS * LS;
-    for (int idx = tid; idx < LAT_ROWS * L; idx += 256) {
+    for (int idx = tid; idx < LAT_ROWS * L; idx += 64 * NWV) {
         const int row = idx / L, col = idx - row * L;
         zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
     }
     __syncthreads();
     const int nct = L / 32, ndt = (N + 31) / 32;
     for (int k = 0; k < a.H; ++k) {
-        // z <- z K: output column tiles ct = wv, wv + 4, ...
-        for (int ct = wv; ct < nct; ct += 4) {
+        // z <- z K: output column tiles ct = wv, wv + NWV, ...
+        for (int ct = wv; ct < nct; ct += NWV) {
             f32x16 acc;
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
@@ -476,19 +480,21 @@ __global__ void __launch_bounds__(256) latent_steps_kernel(LatentArgs a) {
                 zn[((i & 3) + 8 * (i >> 2) + 4 * h) * LS + ct * 32 + (lane & 31)] = acc[i];
         }
         __syncthreads();
-        if (a.ball) {   // x / ||x||_2 per row: 8 threads per row
-            const int row = tid >> 3, part = tid & 7;
-            float sq = 0.0f;
-            for (int j = part; j < L; j += 8) sq += zn[row * LS + j] * zn[row * LS + j];
-            sq += __shfl_xor(sq, 1, 64);
-            sq += __shfl_xor(sq, 2, 64);
-            sq += __shfl_xor(sq, 4, 64);
-            const float nrm = sqrtf(sq);
-            for (int j = part; j < L; j += 8) zn[row * LS + j] = zn[row * LS + j] / nrm;
+        if (a.ball) {   // x / ||x||_2 per row: 8 threads per row (the first 256 threads)
+            if (tid < 8 * LAT_ROWS) {
+                const int row = tid >> 3, part = tid & 7;
+                float sq = 0.0f;
+                for (int j = part; j < L; j += 8) sq += zn[row * LS + j] * zn[row * LS + j];
+                sq += __shfl_xor(sq, 1, 64);
+                sq += __shfl_xor(sq, 2, 64);
+                sq += __shfl_xor(sq, 4, 64);
+                const float nrm = sqrtf(sq);
+                for (int j = part; j < L; j += 8) zn[row * LS + j] = zn[row * LS + j] / nrm;
+            }
             __syncthreads();
         }
         // decode rows 0..N-1 (+ bias), de-standardize into yhat[:, k, :]
-        for (int ct = wv; ct < ndt; ct += 4) {
+        for (int ct = wv; ct < ndt; ct += NWV) {
             f32x16 acc;
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
@@ -530,14 +536,20 @@ __device__ __forceinline__ void tile_dot16(const float* As, int lda, const float
     }
 }
 
-__global__ void __launch_bounds__(256) latent_steps16_kernel(LatentArgs a) {
+// NWV waves per block: the L / 16 column tiles of z K spread over them (8 waves: one tile each at
+// L = 128, two waves per SIMD at configs[1]'s 256 blocks)
+#ifndef KMPC_LAT16_WAVES
+#define KMPC_LAT16_WAVES 8
+#endif
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) {
     extern __shared__ float zs[];   // [2][16][L + 4]
     const int L = a.L, LS = L + 4, N = a.N;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int m0 = blockIdx.x * LAT16;
     float* zc = zs;
     float* zn = zs + LAT16 * LS;
-    for (int idx = tid; idx < LAT16 * L; idx += 256) {
+    for (int idx = tid; idx < LAT16 * L; idx += 64 * NWV) {
         const int row = idx / L, col = idx - row * L;
         zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
     }
@@ -545,26 +557,28 @@ __global__ void __launch_bounds__(256) latent_steps16_kernel(LatentArgs a) {
     const int nct = L / 16, ndt = (N + 15) / 16;
     const int c = lane & 15, rq = 4 * (lane >> 4);
     for (int k = 0; k < a.H; ++k) {
-        for (int ct = wv; ct < nct; ct += 4) {
+        for (int ct = wv; ct < nct; ct += NWV) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             tile_dot16(zc, LS, a.Kt + (size_t)ct * 16 * L, L, true, lane, acc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) zn[(rq + i) * LS + ct * 16 + c] = acc[i];
         }
         __syncthreads();
-        if (a.ball) {   // x / ||x||_2 per row: 16 threads per row
-            const int row = tid >> 4, part = tid & 15;
-            float sq = 0.0f;
-            for (int j = part; j < L; j += 16) sq += zn[row * LS + j] * zn[row * LS + j];
-            sq += __shfl_xor(sq, 1, 64);
-            sq += __shfl_xor(sq, 2, 64);
-            sq += __shfl_xor(sq, 4, 64);
-            sq += __shfl_xor(sq, 8, 64);
-            const float nrm = sqrtf(sq);
-            for (int j = part; j < L; j += 16) zn[row * LS + j] = zn[row * LS + j] / nrm;
+        if (a.ball) {   // x / ||x||_2 per row: 16 threads per row (the first 256 threads)
+            if (tid < 16 * LAT16) {
+                const int row = tid >> 4, part = tid & 15;
+                float sq = 0.0f;
+                for (int j = part; j < L; j += 16) sq += zn[row * LS + j] * zn[row * LS + j];
+                sq += __shfl_xor(sq, 1, 64);
+                sq += __shfl_xor(sq, 2, 64);
+                sq += __shfl_xor(sq, 4, 64);
+                sq += __shfl_xor(sq, 8, 64);
+                const float nrm = sqrtf(sq);
+                for (int j = part; j < L; j += 16) zn[row * LS + j] = zn[row * LS + j] / nrm;
+            }
             __syncthreads();
         }
-        for (int ct = wv; ct < ndt; ct += 4) {
+        for (int ct = wv; ct < ndt; ct += NWV) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             const int nrow = ct * 16 + c;
             tile_dot16(zn, LS, a.D + (size_t)ct * 16 * L, L, nrow < N, lane, acc);
@@ -779,11 +793,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         la.ball = d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL;
         if (Bn < 256 * LAT_ROWS) {   // 16 windows per block: twice the blocks of the 32-row kernel
             const size_t lds = sizeof(float) * 2 * LAT16 * (L + 4);
-            hipLaunchKernelGGL(latent_steps16_kernel, dim3((Bn + LAT16 - 1) / LAT16), dim3(256), lds, s, la);
+            hipLaunchKernelGGL(latent_steps16_kernel<KMPC_LAT16_WAVES>, dim3((Bn + LAT16 - 1) / LAT16),
+                               dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
         const size_t lds = sizeof(float) * 2 * LAT_ROWS * (L + 4);
-        hipLaunchKernelGGL(latent_steps_kernel, dim3((Bn + LAT_ROWS - 1) / LAT_ROWS), dim3(256), lds, s, la);
+        hipLaunchKernelGGL(latent_steps_kernel<KMPC_LAT_WAVES>, dim3((Bn + LAT_ROWS - 1) / LAT_ROWS),
+                           dim3(64 * KMPC_LAT_WAVES), lds, s, la);
         return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
     }
     float* zc = z0;
