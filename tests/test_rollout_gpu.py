@@ -256,3 +256,28 @@ def test_small_batch_split_k_encoder_matches_numpy():
     km.fuse_latent = False
     yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
     assert np.abs(y - yu).max() <= 1e-5 * np.abs(yu).max()
+
+
+@pytest.mark.parametrize("B", [1000, 8200])
+def test_encoder_gemm_tiles_match_numpy(B):
+    """The fp32 GEMM tiles of the encoder at C3's layer widths (obs 400 -> 1024 -> 1024 -> latent 256,
+    N = 100, H = 3): B = 1,000 runs the mid-size path (fewer than 512 128 x 128 tiles: 4 x 4 waves of
+    32 x 32), B = 8,200 the large path (4 x 2 waves of 32 x 64) with a ragged last row tile and a
+    K tail (400 = 12.5 k-tiles). Against the numpy fp32 restatement."""
+    import bench
+    N, L, H, hidden = 100, 256, 3, 1024
+    obs = N * 4
+    sd = bench.make_state_dict(obs, L, hidden, seed=4)
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), torch.device("cuda"))
+    x = torch.randn(B, obs, generator=torch.Generator().manual_seed(5))
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    y = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
+    sdn = {k: v.numpy() for k, v in sd.items()}
+    spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
+               "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],
+               "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None],
+               "norm_fn": bench.MODEL_CFG["MODEL"]["NORM_FN"]}
+    ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
+    dec = ref - mean
+    assert np.abs(y - ref).max() <= 1e-4 * np.abs(dec).max()
