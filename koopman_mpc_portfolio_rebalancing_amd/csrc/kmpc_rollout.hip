@@ -308,7 +308,14 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
 
     const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
                         ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
-    for (int k0 = 0; k0 < g.K; k0 += BK) {
+    // split K: slice blockIdx.z of ksplit (whole BK tiles), raw partials as gemm_nt_kernel
+    int kbeg = 0, kend = g.K;
+    if (g.ksplit > 1) {
+        const int kc = ((g.K + g.ksplit * BK - 1) / (g.ksplit * BK)) * BK;
+        kbeg = blockIdx.z * kc;
+        kend = min(g.K, kbeg + kc);
+    }
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int idx = tid + q * 256;          // 0..1023: 128 rows x 8 groups of 4 k
@@ -316,13 +323,13 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
             const int kk = k0 + c4;
             f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
             const int ma = m0 + row, nb = n0 + row;
-            if (vec_ok && kk + 3 < g.K) {
+            if (vec_ok && kk + 3 < kend) {
                 if (ma < g.M) va = *(const f32x4*)(g.A + (size_t)ma * g.lda + kk);
                 if (nb < g.N) vb = *(const f32x4*)(g.B + (size_t)nb * g.ldb + kk);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (kk + e < g.K) {
+                    if (kk + e < kend) {
                         if (ma < g.M) va[e] = g.A[(size_t)ma * g.lda + kk + e];
                         if (nb < g.N) vb[e] = g.B[(size_t)nb * g.ldb + kk + e];
                     }
@@ -351,6 +358,22 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
         }
         __syncthreads();
+    }
+    if (g.ksplit > 1) {   // raw partial of this K slice
+        float* P = g.part + (size_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int n = n0 + wn + b * 32 + (lane & 31);
+                if (n >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < g.M) P[(size_t)m * g.N + n] = acc[a][b][r];
+                }
+            }
+        return;
     }
     epilogue<2, 2>(g, acc, m0, n0, wm, wn, lane);
 }
@@ -618,6 +641,9 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 #ifndef KMPC_GEMM_MID
 #define KMPC_GEMM_MID 44
 #endif
+#ifndef KMPC_BF16_SPLITK
+#define KMPC_BF16_SPLITK 1
+#endif
 #ifndef KMPC_GEMM_BIG   // tile of the large GEMMs: 22 = 128 x 128 (4 waves), 42 (8 waves), 82 = 256 x 128 (16 waves)
 #define KMPC_GEMM_BIG 42
 #endif
@@ -626,6 +652,17 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
     g.ksplit = 1;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
     if (g.bf16) {
+        // fewer 128 x 128 tiles than CUs (BASELINE configs[4]: 1,024 windows x 512 -> 32 tiles) with a
+        // long K: SPLITK slices, summed in slice order by the epilogue kernel (deterministic)
+        if (KMPC_BF16_SPLITK && part && (size_t)grid.x * grid.y < 256 && g.K >= 128 * SPLITK &&
+            (size_t)g.M * g.N <= SPLITK_ELEMS) {
+            g.ksplit = SPLITK;
+            g.part = part;
+            hipLaunchKernelGGL(gemm_nt_bf16_kernel, dim3(grid.x, grid.y, SPLITK), dim3(256), 0, s, g);
+            const size_t n = (size_t)g.M * g.N;
+            hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+            return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+        }
         hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
     } else if ((size_t)grid.x * grid.y < 512) {
         dim3 grid64((g.N + 63) / 64, (g.M + 63) / 64);
