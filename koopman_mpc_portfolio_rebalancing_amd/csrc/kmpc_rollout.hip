@@ -291,18 +291,22 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmArgs g) {
 // A[row r][k = 8h + j] and B[col r][k = 8h + j], j = 0..7: one ds_read_b128 per operand per step.
 constexpr int LDS_STRIDE_H = BK + 8;   // bf16 elements per LDS row (80 B: 16-B aligned fragments)
 
+// WT = 2: 128 x 128 tile (4 waves of 64 x 64); WT = 1: 64 x 64 (4 waves of 32 x 32), for grids with
+// fewer 128-tiles than CUs and a short K (configs[4]'s LISTA and latent-step layers)
+template <int WT>
 __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
-    __shared__ __bf16 As[BM * LDS_STRIDE_H];
-    __shared__ __bf16 Bs[BN * LDS_STRIDE_H];
+    constexpr int TM = 64 * WT;
+    __shared__ __bf16 As[TM * LDS_STRIDE_H];
+    __shared__ __bf16 Bs[TM * LDS_STRIDE_H];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int m0, n0;
-    xcd_tile(m0, n0);
-    const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
-    f32x16 acc[2][2];
+    xcd_tile(m0, n0, TM, TM);
+    const int wm = (wv >> 1) * 32 * WT, wn = (wv & 1) * 32 * WT;
+    f32x16 acc[WT][WT];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < WT; ++b)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
@@ -317,8 +321,8 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
     }
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int idx = tid + q * 256;          // 0..1023: 128 rows x 8 groups of 4 k
+        for (int q = 0; q < 2 * WT; ++q) {
+            const int idx = tid + q * 256;          // TM rows x 8 groups of 4 k
             const int row = idx >> 3, c4 = (idx & 7) * 4;
             const int kk = k0 + c4;
             f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
@@ -345,16 +349,16 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
         const int r = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int st = 0; st < BK / 16; ++st) {
-            bf16x8 af[2], bfr[2];
+            bf16x8 af[WT], bfr[WT];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) {
+            for (int a = 0; a < WT; ++a) {
                 af[a] = *(const bf16x8*)(As + (wm + a * 32 + r) * LDS_STRIDE_H + 16 * st + 8 * h);
                 bfr[a] = *(const bf16x8*)(Bs + (wn + a * 32 + r) * LDS_STRIDE_H + 16 * st + 8 * h);
             }
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < WT; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
+                for (int b = 0; b < WT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
         }
         __syncthreads();
@@ -362,9 +366,9 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
     if (g.ksplit > 1) {   // raw partial of this K slice
         float* P = g.part + (size_t)blockIdx.z * g.M * g.N;
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < WT; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            for (int b = 0; b < WT; ++b) {
                 const int n = n0 + wn + b * 32 + (lane & 31);
                 if (n >= g.N) continue;
 #pragma unroll
@@ -375,7 +379,7 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
             }
         return;
     }
-    epilogue<2, 2>(g, acc, m0, n0, wm, wn, lane);
+    epilogue<WT, WT>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
@@ -631,6 +635,7 @@ static bool latent_fusable(const kmpc_rollout_desc* d) {
 // split-K partial buffer: SPLITK slices of at most SPLITK_ELEMS outputs (split only when the
 // 64 x 64 tiles number fewer than 256, i.e. M N <= 256 * 64 * 64)
 constexpr int SPLITK = 4;
+constexpr int SPLITK_BUF = 8;   // slices the partial buffer holds (the bf16 long-K split uses all 8)
 constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 
 // tile of the mid-size GEMMs (fewer than 512 128-square tiles): 11 = 64 x 64, 21 = 128 x 64,
@@ -644,6 +649,12 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 #ifndef KMPC_BF16_SPLITK
 #define KMPC_BF16_SPLITK 1
 #endif
+#ifndef KMPC_BF16_SPLIT_MINK   // bf16 split-K only for long K (the LISTA encoder's obs = 10,000)
+#define KMPC_BF16_SPLIT_MINK 2048
+#endif
+#ifndef KMPC_BF16_SMALL
+#define KMPC_BF16_SMALL 1
+#endif
 #ifndef KMPC_GEMM_BIG   // tile of the large GEMMs: 22 = 128 x 128 (4 waves), 42 (8 waves), 82 = 256 x 128 (16 waves)
 #define KMPC_GEMM_BIG 42
 #endif
@@ -654,16 +665,19 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
     if (g.bf16) {
         // fewer 128 x 128 tiles than CUs (BASELINE configs[4]: 1,024 windows x 512 -> 32 tiles) with a
         // long K: SPLITK slices, summed in slice order by the epilogue kernel (deterministic)
-        if (KMPC_BF16_SPLITK && part && (size_t)grid.x * grid.y < 256 && g.K >= 128 * SPLITK &&
-            (size_t)g.M * g.N <= SPLITK_ELEMS) {
-            g.ksplit = SPLITK;
+        const bool few = (size_t)grid.x * grid.y < 256;
+        if (KMPC_BF16_SPLITK && few && part && g.K >= KMPC_BF16_SPLIT_MINK && (size_t)g.M * g.N <= SPLITK_ELEMS) {
+            g.ksplit = SPLITK_BUF;
             g.part = part;
-            hipLaunchKernelGGL(gemm_nt_bf16_kernel, dim3(grid.x, grid.y, SPLITK), dim3(256), 0, s, g);
+            hipLaunchKernelGGL(gemm_nt_bf16_kernel<2>, dim3(grid.x, grid.y, SPLITK_BUF), dim3(256), 0, s, g);
             const size_t n = (size_t)g.M * g.N;
             hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
-        hipLaunchKernelGGL(gemm_nt_bf16_kernel, grid, dim3(256), 0, s, g);
+        if (few && KMPC_BF16_SMALL)   // short K: 64 x 64 tiles (4x the workgroups), no partials
+            hipLaunchKernelGGL(gemm_nt_bf16_kernel<1>, dim3((g.N + 63) / 64, (g.M + 63) / 64), dim3(256), 0, s, g);
+        else
+            hipLaunchKernelGGL(gemm_nt_bf16_kernel<2>, grid, dim3(256), 0, s, g);
     } else if ((size_t)grid.x * grid.y < 512) {
         dim3 grid64((g.N + 63) / 64, (g.M + 63) / 64);
         // fewer 64 x 64 tiles than CUs (e.g. the 128-wide last encoder layer of BASELINE configs[1]:
@@ -730,7 +744,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
     bytes += 2 * align256(sizeof(float) * B * wmax);               // ping-pong activations
     bytes += 2 * align256(sizeof(float) * B * d->L);               // z, c (LISTA) / z next
     const size_t part = B * (size_t)wmax < SPLITK_ELEMS ? B * (size_t)wmax : SPLITK_ELEMS;
-    bytes += align256(sizeof(float) * SPLITK * part);              // split-K partials (small batches)
+    bytes += align256(sizeof(float) * SPLITK_BUF * part);          // split-K partials (small batches)
     return bytes;
 }
 
