@@ -10,7 +10,8 @@ if os.environ.get("KMPC_DEV_LIB"):   # a variant library (csrc/Makefile tvar)
     _lib._lib = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["KMPC_DEV_LIB"]))
 
 dev = torch.device("cuda", 0)
-B, N, L, H, hidden = int(os.environ.get("B", "4096")), 30, 128, 5, 1024
+B, N, L, H, hidden = (int(os.environ.get("B", "4096")), int(os.environ.get("N", "30")), int(os.environ.get("LAT", "128")),
+                      int(os.environ.get("H", "5")), 1024)
 obs = N * 20
 model = DeviceKoopman(KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs, L, hidden, seed=1), bench.MODEL_CFG), dev)
 mean_d = torch.full((N,), 5e-4, dtype=torch.float32, device=dev)
