@@ -565,6 +565,9 @@ __device__ __forceinline__ void tile_dot16(const float* As, int lda, const float
 
 // NWV waves per block: the L / 16 column tiles of z K spread over them (8 waves: one tile each at
 // L = 128, two waves per SIMD at configs[1]'s 256 blocks)
+#ifndef KMPC_LAT16_MAXB   // batches below this run the 16-row kernel
+#define KMPC_LAT16_MAXB (256 * 32)
+#endif
 #ifndef KMPC_LAT16_WAVES
 #define KMPC_LAT16_WAVES 8
 #endif
@@ -842,7 +845,10 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
         la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
         la.ball = d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL;
-        if (Bn < 256 * LAT_ROWS) {   // 16 windows per block: twice the blocks of the 32-row kernel
+        // 16 windows per block: twice the blocks of the 32-row kernel for small batches, and one z K
+        // column tile per wave at L <= 128 (65,536 windows, L = 128: 263 -> 184 us; at L = 256 the
+        // 32-row kernel stays ahead: 1,346 vs 1,575 us)
+        if (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES) {
             const size_t lds = sizeof(float) * 2 * LAT16 * (L + 4);
             hipLaunchKernelGGL(latent_steps16_kernel<KMPC_LAT16_WAVES>, dim3((Bn + LAT16 - 1) / LAT16),
                                dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
