@@ -64,10 +64,10 @@ __device__ __forceinline__ int gsumi(int v) {
 // (H independent butterflies interleaved, instead of H dependent rounds). Same arithmetic and order
 // as the general loop below (a group butterfly over G lanes adds zeros where the wave-wide one did):
 // bit-identical results.
-template <int G>
+// HR: the period bound; HX = H known at compile time (BASELINE configs[1]: H = 5 — no period guards)
+template <int G, int HR = SIMPLEX_HR, bool HX = false>
 __device__ __forceinline__ void simplex_regs(const SolveArgs& a, int b, int lane) {
-    constexpr int HR = SIMPLEX_HR;
-    const int N = a.N, H = a.H, tw = a.return_full ? H : 1;
+    const int N = a.N, H = HX ? HR : a.H, tw = a.return_full ? H : 1;
     const float* y = a.yhat + (size_t)b * H * N;
     const double* wp = a.wp + (size_t)b * N;
     double* wout = a.wout + (size_t)b * tw * N;
@@ -157,7 +157,10 @@ __global__ void __launch_bounds__(64 * SIMPLEX_WAVES) simplex_kernel(SolveArgs a
     if (a.N <= 32 && a.H <= SIMPLEX_HR) {
         // two windows per wave, one per 32-lane half
         const int b = (blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-        if (b < a.B) simplex_regs<32>(a, b, lane & 31);   // (whole lane groups)
+        if (b < a.B) {   // (whole lane groups)
+            if (a.H == 5) simplex_regs<32, 5, true>(a, b, lane & 31);
+            else simplex_regs<32>(a, b, lane & 31);
+        }
         return;
     }
     const int b = blockIdx.x * SIMPLEX_WAVES + (threadIdx.x >> 6);
