@@ -433,6 +433,9 @@ __global__ void transpose_kernel(const float* in, float* out, int R, int Cc) {
 struct LatentArgs {
     int B, L, N, H;
     const float* z0;     // [B, L]
+    // z0 as the raw split-K partials of the last encoder layer (nparts > 0): z0 = sum of the parts in
+    // slice order + zbias, as splitk_epilogue_kernel would have formed it (bit-identical)
+    const float* zparts; int nparts; const float* zbias;
     const float* Kt;     // [L, L]: row j = column j of K
     const float* D;      // decoder rows 0..N-1, [N, L]
     const float* bias;   // [N] or null
@@ -441,6 +444,14 @@ struct LatentArgs {
     int ball;
 };
 constexpr int LAT_ROWS = 32;
+
+__device__ __forceinline__ float latent_z0(const LatentArgs& a, int m, int col) {
+    const size_t i = (size_t)m * a.L + col;
+    if (a.nparts == 0) return a.z0[i];
+    float v = a.zparts[i];
+    for (int z = 1; z < a.nparts; ++z) v += a.zparts[(size_t)z * a.B * a.L + i];
+    return v + (a.zbias ? a.zbias[col] : 0.0f);
+}
 
 // acc (+)= A[32 rows of As, stride lda] . B[32 rows of Bg, stride L]^T over k in [0, L)
 __device__ __forceinline__ void tile_dot(const float* As, int lda, const float* Bg, int L, bool brow_ok,
@@ -491,7 +502,7 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps_kernel(LatentArgs a) {
     float* zn = zs + LAT_ROWS * LS;
     for (int idx = tid; idx < LAT_ROWS * L; idx += 64 * NWV) {
         const int row = idx / L, col = idx - row * L;
-        zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
+        zc[row * LS + col] = (m0 + row < a.B) ? latent_z0(a, m0 + row, col) : 0.0f;
     }
     __syncthreads();
     const int nct = L / 32, ndt = (N + 31) / 32;
@@ -581,7 +592,7 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) 
     float* zn = zs + LAT16 * LS;
     for (int idx = tid; idx < LAT16 * L; idx += 64 * NWV) {
         const int row = idx / L, col = idx - row * L;
-        zc[row * LS + col] = (m0 + row < a.B) ? a.z0[(size_t)(m0 + row) * L + col] : 0.0f;
+        zc[row * LS + col] = (m0 + row < a.B) ? latent_z0(a, m0 + row, col) : 0.0f;
     }
     __syncthreads();
     const int nct = L / 16, ndt = (N + 15) / 16;
@@ -652,6 +663,9 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 #ifndef KMPC_BF16_SPLITK
 #define KMPC_BF16_SPLITK 1
 #endif
+#ifndef KMPC_Z0_FUSE   // the last encoder layer's split-K sum folded into the fused latent loop
+#define KMPC_Z0_FUSE 1
+#endif
 #ifndef KMPC_BF16_SPLIT_MINK   // bf16 split-K only for long K (the LISTA encoder's obs = 10,000)
 #define KMPC_BF16_SPLIT_MINK 2048
 #endif
@@ -661,7 +675,10 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 #ifndef KMPC_GEMM_BIG   // tile of the large GEMMs: 22 = 128 x 128 (4 waves), 42 (8 waves), 82 = 256 x 128 (16 waves)
 #define KMPC_GEMM_BIG 42
 #endif
-static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
+// nparts (optional): a split-K layer with no epilogue (EPI_NONE) leaves its raw partials in part and
+// reports the slice count instead of launching splitk_epilogue_kernel (the latent kernels sum them)
+static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr, int* nparts = nullptr) {
+    if (nparts) *nparts = 0;
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     g.ksplit = 1;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
@@ -690,6 +707,10 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr) {
             g.ksplit = SPLITK;
             g.part = part;
             hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), dim3(grid64.x, grid64.y, SPLITK), dim3(256), 0, s, g);
+            if (nparts && g.epi == EPI_NONE) {
+                *nparts = SPLITK;
+                return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+            }
             const size_t n = (size_t)g.M * g.N;
             hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
@@ -755,7 +776,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
 // layer, written with row stride ldo); ping/pong are [B, wmax] scratch buffers.
 static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* out, int ldo,
                    int last_cols, int last_epi, const float* mean, const float* stdv, float* ping,
-                   float* pong, int wmax, int bf16, hipStream_t s, float* part) {
+                   float* pong, int wmax, int bf16, hipStream_t s, float* part, int* last_nparts = nullptr) {
     const float* cur = X;
     int ldc = ldx;
     for (int l = 0; l < m.n_layers; ++l) {
@@ -768,7 +789,7 @@ static int run_mlp(const kmpc_mlp& m, int Bn, const float* X, int ldx, float* ou
         if (!last) { g.epi = EPI_ACT; g.act = m.act; }
         else if (last_epi == EPI_DESTD) { g.epi = EPI_DESTD; g.mean = mean; g.stdv = stdv; }
         else if (m.last_relu) { g.epi = EPI_ACT; g.act = KMPC_ACT_RELU; }
-        int rc = gemm(g, s, part);
+        int rc = gemm(g, s, part, last ? last_nparts : nullptr);
         if (rc) return rc;
         cur = dst;
         ldc = wmax;
@@ -814,8 +835,12 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
 
     // ---- encode ----
+    int znparts = 0;   // > 0: z0 left as split-K partials for the fused latent loop to sum
+    const bool zfuse = KMPC_Z0_FUSE && d->model_kind == KMPC_MODEL_GENERIC && latent_fusable(d) &&
+                       d->norm_fn != KMPC_NORM_BALL;
     if (d->model_kind == KMPC_MODEL_GENERIC) {
-        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s, part);
+        rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s, part,
+                     zfuse ? &znparts : nullptr);
         if (rc) return rc;
         if (d->norm_fn == KMPC_NORM_BALL)
             hipLaunchKernelGGL(ball_norm_kernel, dim3((Bn + 3) / 4), dim3(256), 0, s, z0, Bn, L);
@@ -843,6 +868,8 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (latent_fusable(d)) {
         LatentArgs la;
         la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
+        la.zparts = part; la.nparts = znparts;
+        la.zbias = d->encoder.bias[d->encoder.n_layers - 1];
         la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
         la.ball = d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL;
         // 16 windows per block: twice the blocks of the 32-row kernel for small batches, and one z K
