@@ -28,6 +28,8 @@ int big_launch(const SolveArgs& a, void* ws, size_t ws_size, hipStream_t stream)
 // constant-case kernels (kmpc_solve_h*_case.hip); KMPC_ERR_UNSUPPORTED if the case has none
 template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream);
+// the C3 kernel (H = 10, FL = 7, 128 threads, LDL^T arrays in LDS) in its own -O2 unit (kmpc_solve_c3.hip)
+int launch_ipm_c3(const SolveArgs& a, hipStream_t stream);
 // packed small-window kernels, 64 / GL windows per wave (kmpc_solve_p*.hip); KMPC_ERR_UNSUPPORTED
 // outside N <= 32, 3 H <= 32
 template <int HM>

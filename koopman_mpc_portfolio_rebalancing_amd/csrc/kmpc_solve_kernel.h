@@ -1980,7 +1980,7 @@ int launch_ipm_case(const SolveArgs& a, hipStream_t stream) {
         // join the cold arrays in LDS with a 104-lane stride (two windows per CU still fit):
         // 40 VGPRs of live state less, 132 -> 107 spilled dwords, C3 solve +4.5% (measured r02)
         if constexpr (HM == 10) {
-            if (nt == 128 && a.N < QL_CS) return launch_one<HM, 128, true, 7, QL_CS, true>(a, nt, stream);
+            if (nt == 128 && a.N < QL_CS) return launch_ipm_c3(a, stream);
             // 256-thread windows (one per CU): the 8 cold arrays at a 216-lane stride fit 160 KB
             // (151 -> 108 spilled dwords; N = 200 +6.7%, measured r02)
             if (nt == 256 && a.N < QL_CS256) return launch_one<HM, 256, true, 7, QL_CS256, true>(a, nt, stream);

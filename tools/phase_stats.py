@@ -8,7 +8,7 @@ from koopman_mpc_portfolio_rebalancing_amd import _lib, MPCConfig, solve_mpc_log
 def read_stats(L, reset=1):
     """Sum of the dev counters of every solve translation unit that exports a reader."""
     tot = [0] * 18
-    for fn in ("kmpc_debug_stats", "kmpc_debug_stats_case"):
+    for fn in ("kmpc_debug_stats", "kmpc_debug_stats_case", "kmpc_debug_stats_c3"):
         if hasattr(L, fn):
             f = getattr(L, fn)
             f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]

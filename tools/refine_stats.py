@@ -10,7 +10,7 @@ from oracle import solver as oracle
 def read_stats(L, reset=1):
     """Sum of the dev counters of every solve translation unit that exports a reader."""
     tot = [0] * 18
-    for fn in ("kmpc_debug_stats", "kmpc_debug_stats_case"):
+    for fn in ("kmpc_debug_stats", "kmpc_debug_stats_case", "kmpc_debug_stats_c3"):
         if hasattr(L, fn):
             f = getattr(L, fn)
             f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
