@@ -60,7 +60,8 @@ def test_dmd_rollout_and_solve_match_reference_calls():
     T = g["call_yhat"].shape[0]
     y = km.rollout(torch.from_numpy(g["test_data"][:T]).cuda(), g["mean"], g["std"], meta["H"], meta["N"]).cpu().numpy()
     ref = g["call_yhat"]
-    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+    print(f"[rel] dmd {np.abs(y - ref).max() / np.abs(ref).max():.3e}")
+    assert np.abs(y - ref).max() <= 2e-6 * np.abs(ref).max()   # measured 1.9e-7 on MI355X
     W0 = strat.rebalance_batch(list(range(T)), g["call_wprev"], env)
     assert np.abs(W0 - g["call_W"][:, 0]).max() < 1e-3
     # the per-window drop-in (backtest.py / baselines.py signature) agrees with the batched path

@@ -2,8 +2,9 @@
 model.py (tests/golden), plus the fused window and the end-to-end backtest.
 
 Rollout tolerance: fp32 arithmetic like the reference; the MFMA dot products sum in a different
-order, so |yhat - ref| <= 1e-4 * max|ref| (measured ~1e-6 relative).
-"""
+order. Bars (max|yhat - ref| / max|ref|, printed by assert_rel under pytest -s): 2e-6 against the
+reference-generated goldens (measured 0.6-3.0e-7 on MI355X), 1e-5 against the numpy fp32
+restatement and between launch variants (measured <= 1.3e-6)."""
 import glob
 import json
 import os
@@ -22,6 +23,13 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+def assert_rel(d, scale, tol, what=""):
+    """max|d| <= tol * scale; prints the measured ratio (pytest -s) so the bar can be checked."""
+    r = float(np.abs(d).max()) / float(scale)
+    print(f"[rel] {what} {r:.3e} (bar {tol:.0e})")
+    assert r <= tol, (what, r, tol)
+
+
 def load_spec(g):
     meta = json.loads(str(g["meta"]))
     sd = {k[2:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w:")}
@@ -36,7 +44,7 @@ def test_rollout_matches_reference(path):
     y = km.rollout(torch.from_numpy(g["obs"]).cuda(), g["mean"], g["std"], meta["H"], meta["N"]).cpu().numpy()
     ref = g["yhat"]
     assert y.shape == ref.shape
-    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert_rel(y - ref, np.abs(ref).max(), 2e-6, os.path.basename(path))
 
 
 def test_rollout_large_batch_matches_numpy_restatement():
@@ -52,7 +60,7 @@ def test_rollout_large_batch_matches_numpy_restatement():
                "enc_b": [sd[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sd["kmat"],
                "dec_w": [sd["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": "id"}
     ref = R.rollout(spec_np, obs, 7, meta["N"], g["mean"].astype(np.float32), g["std"].astype(np.float32))
-    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert_rel(y - ref, np.abs(ref).max(), 1e-5, "large batch")
 
 
 def test_fused_window_equals_rollout_then_solve():
@@ -88,7 +96,7 @@ def test_backtest_matches_reference_run():
     T = g["call_yhat"].shape[0]
     y = km.rollout(torch.from_numpy(g["test_data"][:T]).cuda(), g["mean"], g["std"], meta["H"], meta["N"])
     ref_y = g["call_yhat"]
-    assert np.abs(y.cpu().numpy() - ref_y).max() <= 1e-4 * np.abs(ref_y).max()
+    assert_rel(y.cpu().numpy() - ref_y, np.abs(ref_y).max(), 2e-6, "backtest call_yhat")
     df = run_backtest(strat, env, BacktestConfig(**meta["backtest"]), verbose=False)
     assert len(df) == len(g["df_value"])
     np.testing.assert_allclose(df["portfolio_value"].values, g["df_value"], rtol=1e-6)
@@ -126,7 +134,7 @@ def test_panel_rollout_equals_embedded_rollout():
     for first, nwin in ((0, emb.shape[0]), (5, 11)):
         y_pan = km.rollout_panel(zt, d, first, nwin, mean, std, H, N).cpu().numpy()
         ref = y_emb[first:first + nwin]
-        assert np.abs(y_pan - ref).max() <= 1e-5 * np.abs(ref).max()
+        assert_rel(y_pan - ref, np.abs(ref).max(), 1e-5, "panel")
     with pytest.raises(ValueError):
         km.rollout_panel(zt, d, T - d, 2, mean, std, H, N)
 
@@ -190,7 +198,7 @@ def test_bf16_lista_rollout_at_config5_shape():
     # fp32 chain first: the same kernels and data path, exact fp32 products -> summation order only
     y32 = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
     ref32 = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
-    assert np.abs(y32 - ref32).max() <= 1e-4 * np.abs(ref32).max()
+    assert_rel(y32 - ref32, np.abs(ref32).max(), 1e-5, "lista fp32")
     # bf16 chain: 30 dependent roundings of the state to bf16 (10 LISTA loops, 20 K steps); a
     # summation-order difference of ~1e-6 flips an occasional element's rounding (1 bf16 ulp =
     # 2^-8 relative) and the flips propagate — measured ~4e-3 normwise against the bf16-operand
@@ -226,8 +234,8 @@ def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
                "enc_b": [sdn[f"encoder.network.{i}.bias"] for i in (0, 2, 4)], "kmat": sdn["kmat"],
                "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": norm}
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
-    assert np.abs(yf - ref).max() <= 1e-4 * np.abs(ref).max()
-    assert np.abs(yf - yu).max() <= 1e-5 * np.abs(yu).max()
+    assert_rel(yf - ref, np.abs(ref).max(), 1e-5, f"fused {norm} L{L} B{B}")
+    assert_rel(yf - yu, np.abs(yu).max(), 1e-5, f"fused-vs-unfused {norm} L{L} B{B}")
 
 
 def test_small_batch_split_k_encoder_matches_numpy():
@@ -252,10 +260,10 @@ def test_small_batch_split_k_encoder_matches_numpy():
                "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None],
                "norm_fn": bench.MODEL_CFG["MODEL"]["NORM_FN"]}
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
-    assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert_rel(y - ref, np.abs(ref).max(), 1e-5, "configs[1] split-K")
     km.fuse_latent = False
     yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
-    assert np.abs(y - yu).max() <= 1e-5 * np.abs(yu).max()
+    assert_rel(y - yu, np.abs(yu).max(), 1e-5, "configs[1] fused-vs-unfused")
 
 
 @pytest.mark.parametrize("B", [1000, 8200])
@@ -280,4 +288,4 @@ def test_encoder_gemm_tiles_match_numpy(B):
                "norm_fn": bench.MODEL_CFG["MODEL"]["NORM_FN"]}
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
     dec = ref - mean
-    assert np.abs(y - ref).max() <= 1e-4 * np.abs(dec).max()
+    assert_rel(y - ref, np.abs(dec).max(), 1e-5, f"encoder tiles B{B}")

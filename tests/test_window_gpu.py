@@ -122,7 +122,7 @@ def test_fp32_window_n300_h12_equals_rollout_then_solve():
                "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": "ball"}
     ref = R.rollout(spec_np, x[:128].cpu().numpy(), H, N, mean, std)
     yn = y[:128].cpu().numpy()
-    assert np.abs(yn - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert np.abs(yn - ref).max() <= 1e-5 * np.abs(ref).max()   # measured <= 1.3e-6 (test_rollout_gpu.py)
     _check_against_oracle(W0.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy(), wp.cpu().numpy(),
                           y.cpu().numpy(), cfg, np.array([0, 512, B - 1]))
 
@@ -150,7 +150,7 @@ def test_config0_model_rollout_and_window():
     ref = R.rollout(spec_np, x.cpu().numpy(), H, N, mean, std)
     yn = y.cpu().numpy()
     assert yn.shape == (B, H, N)
-    assert np.abs(yn - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert np.abs(yn - ref).max() <= 1e-5 * np.abs(ref).max()   # measured <= 1.3e-6 (test_rollout_gpu.py)
     cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
     W0, st, val = km.window(x, wp, mean, std, N, cfg)
     W0b, stb, valb = solve_mpc_log_utility_batched(wp, y, cfg)
