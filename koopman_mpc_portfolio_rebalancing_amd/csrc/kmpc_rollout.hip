@@ -436,7 +436,8 @@ struct LatentArgs {
     // z0 as the raw split-K partials of the last encoder layer (nparts > 0): z0 = sum of the parts in
     // slice order + zbias, as splitk_epilogue_kernel would have formed it (bit-identical)
     const float* zparts; int nparts; const float* zbias;
-    const float* Kt;     // [L, L]: row j = column j of K
+    const float* Kt;     // [L, L]: row j = column j of K (32-row kernel)
+    const float* K;      // [L, L] row-major, z <- z K (16-row kernel: read in place, no transpose launch)
     const float* D;      // decoder rows 0..N-1, [N, L]
     const float* bias;   // [N] or null
     const float* mean; const float* stdv;
@@ -574,6 +575,27 @@ __device__ __forceinline__ void tile_dot16(const float* As, int lda, const float
     }
 }
 
+// tile_dot16 with B = columns col0.. col0 + 15 of the row-major K read in place: lane (r, kq) loads
+// K[k0 + 4 kq + e][col0 + r], e = 0..3 (16 lanes cover 64 contiguous bytes of a K row; K is L2
+// resident). Same values and k order as tile_dot16 on K^T, so the sums are bit-identical.
+__device__ __forceinline__ void tile_dot16_k(const float* As, int lda, const float* K, int col0, int L, int lane,
+                                             f32x4& acc) {
+    const int r = lane & 15, kq = lane >> 4;
+    const float* pa = As + r * lda + 4 * kq;
+    const float* pb = K + (size_t)(4 * kq) * L + col0 + r;
+    f32x4 bn = {pb[0], pb[L], pb[2 * L], pb[3 * L]};
+    for (int k0 = 0; k0 < L; k0 += 16) {
+        const f32x4 av = *(const f32x4*)(pa + k0);
+        const f32x4 bv = bn;
+        if (k0 + 16 < L) {
+            const float* q = pb + (size_t)(k0 + 16) * L;
+            bn = f32x4{q[0], q[L], q[2 * L], q[3 * L]};
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
+    }
+}
+
 // NWV waves per block: the L / 16 column tiles of z K spread over them (8 waves: one tile each at
 // L = 128, two waves per SIMD at configs[1]'s 256 blocks)
 #ifndef KMPC_LAT16_MAXB   // batches below this run the 16-row kernel
@@ -582,7 +604,7 @@ __device__ __forceinline__ void tile_dot16(const float* As, int lda, const float
 #ifndef KMPC_LAT16_WAVES
 #define KMPC_LAT16_WAVES 8
 #endif
-template <int NWV>
+template <int NWV, bool KDIR>
 __global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) {
     extern __shared__ float zs[];   // [2][16][L + 4]
     const int L = a.L, LS = L + 4, N = a.N;
@@ -600,7 +622,8 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) 
     for (int k = 0; k < a.H; ++k) {
         for (int ct = wv; ct < nct; ct += NWV) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            tile_dot16(zc, LS, a.Kt + (size_t)ct * 16 * L, L, true, lane, acc);
+            if (KDIR) tile_dot16_k(zc, LS, a.K, ct * 16, L, lane, acc);
+            else tile_dot16(zc, LS, a.Kt + (size_t)ct * 16 * L, L, true, lane, acc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) zn[(rq + i) * LS + ct * 16 + c] = acc[i];
         }
@@ -828,8 +851,13 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     float* z1 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
     float* part = (float*)p;   // split-K partials (gemm(): only M N <= SPLITK_ELEMS outputs are split)
     int rc;
+    // Small batches (the fused 16-row latent loop below KMPC_LAT16_MAXB windows) read K in place and
+    // skip the transpose launch (configs[1]: 0.194 -> 0.190 ms per step); at 65,536 windows the
+    // in-place read costs the latent loop more than the launch, so K^T stays (A/B).
+    const bool lat16 = latent_fusable(d) && (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES);
+    const bool kdir = lat16 && Bn < KMPC_LAT16_MAXB;
     dim3 tg((L + 31) / 32, (L + 31) / 32);
-    hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
+    if (!kdir) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
     if (d->model_kind == KMPC_MODEL_LISTA)
         hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->lista_S, St, L, L);
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
@@ -867,7 +895,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     // ---- H x (step_latent, decode[:N], destandardize) ----
     if (latent_fusable(d)) {
         LatentArgs la;
-        la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.D = d->decoder.weight[0];
+        la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.K = d->kmat; la.D = d->decoder.weight[0];
         la.zparts = part; la.nparts = znparts;
         la.zbias = d->encoder.bias[d->encoder.n_layers - 1];
         la.bias = d->decoder.bias[0]; la.mean = d->mean; la.stdv = d->std; la.yhat = yhat;
@@ -875,10 +903,14 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         // 16 windows per block: twice the blocks of the 32-row kernel for small batches, and one z K
         // column tile per wave at L <= 128 (65,536 windows, L = 128: 263 -> 184 us; at L = 256 the
         // 32-row kernel stays ahead: 1,346 vs 1,575 us)
-        if (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES) {
+        if (lat16) {
             const size_t lds = sizeof(float) * 2 * LAT16 * (L + 4);
-            hipLaunchKernelGGL(latent_steps16_kernel<KMPC_LAT16_WAVES>, dim3((Bn + LAT16 - 1) / LAT16),
-                               dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
+            if (kdir)
+                hipLaunchKernelGGL((latent_steps16_kernel<KMPC_LAT16_WAVES, true>), dim3((Bn + LAT16 - 1) / LAT16),
+                                   dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
+            else
+                hipLaunchKernelGGL((latent_steps16_kernel<KMPC_LAT16_WAVES, false>), dim3((Bn + LAT16 - 1) / LAT16),
+                                   dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
         const size_t lds = sizeof(float) * 2 * LAT_ROWS * (L + 4);

@@ -29,6 +29,8 @@ torch.cuda.synchronize()
 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 e[0].record(); y = model.rollout(x, mean_d, std_d, H, N); e[1].record(); solve_mpc_log_utility_batched(wp, y, cfg); e[2].record()
 torch.cuda.synchronize()
+import hashlib
+print("yhat sha1", hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:16], flush=True)
 print(f"eager kernels: rollout {e[0].elapsed_time(e[1]):.3f} ms, solve {e[1].elapsed_time(e[2]):.3f} ms", flush=True)
 reps = 200
 t0 = time.perf_counter()
