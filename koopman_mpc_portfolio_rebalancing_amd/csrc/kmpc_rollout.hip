@@ -671,7 +671,10 @@ static bool latent_fusable(const kmpc_rollout_desc* d) {
 
 // split-K partial buffer: SPLITK slices of at most SPLITK_ELEMS outputs (split only when the
 // 64 x 64 tiles number fewer than 256, i.e. M N <= 256 * 64 * 64)
-constexpr int SPLITK = 4;
+#ifndef KMPC_F32_SPLITK   // K slices of the fp32 split-K GEMM (<= SPLITK_BUF)
+#define KMPC_F32_SPLITK 4
+#endif
+constexpr int SPLITK = KMPC_F32_SPLITK;
 constexpr int SPLITK_BUF = 8;   // slices the partial buffer holds (the bf16 long-K split uses all 8)
 constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 
@@ -726,6 +729,7 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr, int* nparts = 
         // fewer 64 x 64 tiles than CUs (e.g. the 128-wide last encoder layer of BASELINE configs[1]:
         // 4,096 x 128 -> 128 tiles) with a long K: split K in SPLITK slices (4 x the workgroups), the
         // partials summed in slice order by the epilogue kernel (deterministic)
+        static_assert(SPLITK >= 2 && SPLITK <= SPLITK_BUF, "split-K slices");
         if (part && (size_t)grid64.x * grid64.y < 256 && g.K >= 128 * SPLITK) {
             g.ksplit = SPLITK;
             g.part = part;
