@@ -73,6 +73,8 @@ extern "C" {
  *          kernel keeps each window's interior-point state there: (22 HM + 128) (64 ceil(N / 64))
  *          doubles per window slot, HM = 10 for H <= 10 and 21 past it (the compiled horizon
  *          bound, not H), for min(B, 768) slots when N <= 256, min(B, 512) otherwise.
+ *          The mixed-precision pair (KMPC_PRECISION_AUTO) keeps one float32 iterate record per
+ *          window of a chunk of min(B, 131072) windows: (5 H N + 3 H + 16) floats rounded up to 64 B.
  *          Too little -> KMPC_ERR_WORKSPACE.
  */
 #define KMPC_PATH_AUTO     0   /* kernel chosen by shape (and the closed-form presolve)            */
@@ -80,6 +82,13 @@ extern "C" {
 #define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
 #define KMPC_PATH_REGISTER_UNPACKED 3   /* register kernels, one window per wave even for N <= 32
                                            (no lane-group packing); for A/B and tests             */
+/* Arithmetic of the interior point. AUTO: where a mixed-precision kernel pair exists (H = 10,
+ * N <= 103, no short, c > 0 or tau > 0 with a cap: BASELINE configs[2..3]) the first iterations run
+ * in float32 (half the registers, two waves per SIMD) until mu <= mu_handoff, and the float64 kernel
+ * finishes from that iterate to the same tolerance and status rules as F64; elsewhere float64.
+ * F64: float64 throughout. The answer's accuracy is that of the float64 finish either way. */
+#define KMPC_PRECISION_AUTO 0
+#define KMPC_PRECISION_F64  1
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */
@@ -93,6 +102,10 @@ typedef struct kmpc_solve_desc {
     int    n_refine;       /* max iterative-refinement steps per Newton solve; refinement stops once
                               ||r||_inf <= 1e-7 ||b||_inf (<0 -> none, 0 -> default 3)             */
     int    path;           /* KMPC_PATH_* (0 = by shape). Per call: no process-wide switches      */
+    int    precision;      /* KMPC_PRECISION_* (ABI 0.3.0)                                        */
+    double mu_handoff;     /* mixed precision: the float32 phase hands its iterate to the float64
+                              solve once the scaled complementarity mu <= mu_handoff
+                              (<= 0 -> default 1e-4)                                               */
 } kmpc_solve_desc;
 
 int kmpc_solve(const kmpc_solve_desc* desc,
@@ -269,7 +282,8 @@ size_t kmpc_workspace_bytes(const kmpc_rollout_desc* rdesc, const kmpc_solve_des
 const char* kmpc_strerror(int code);
 
 /* Library version string, "kmpc <ABI> (gfx950)". ABI 0.2.0 appended kmpc_solve_desc.path and
-   kmpc_rollout_desc.latent_unfused: callers built against 0.1.0 must rebuild. */
+   kmpc_rollout_desc.latent_unfused; 0.3.0 appended kmpc_solve_desc.precision and .mu_handoff:
+   callers built against an older ABI must rebuild. */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

@@ -36,10 +36,12 @@ EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace
                     "kmpc_mv_workspace_bytes", "kmpc_gross_returns")
 
 PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
+PRECISION_AUTO, PRECISION_F64 = 0, 1   # kmpc_solve_desc.precision
 
 # ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
-# kmpc_rollout_desc.latent_unfused, so an older library would read them past its structs' end
-ABI_VERSION = "0.2.0"
+# kmpc_rollout_desc.latent_unfused, 0.3.0 kmpc_solve_desc.precision and .mu_handoff, so an older
+# library would read them past its structs' end
+ABI_VERSION = "0.3.0"
 
 
 class KmpcError(RuntimeError):
@@ -51,7 +53,7 @@ class SolveDesc(ctypes.Structure):
                 ("cost_coeff", ctypes.c_double), ("max_turnover", ctypes.c_double),
                 ("allow_short", ctypes.c_int), ("max_iter", ctypes.c_int),
                 ("tol", ctypes.c_double), ("return_full_W", ctypes.c_int), ("n_refine", ctypes.c_int),
-                ("path", ctypes.c_int)]
+                ("path", ctypes.c_int), ("precision", ctypes.c_int), ("mu_handoff", ctypes.c_double)]
 
 
 class MvDesc(ctypes.Structure):

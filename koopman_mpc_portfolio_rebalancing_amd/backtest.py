@@ -207,7 +207,7 @@ METRIC_NAMES = ("Sharpe Ratio", "Max Drawdown", "Avg Turnover", "Final Value", "
 
 
 def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
-                          mean, std, n_rows: Optional[int] = None) -> Dict[str, Any]:
+                          mean, std, n_rows: Optional[int] = None, graph: bool = False) -> Dict[str, Any]:
     """P independent backtests of the reference loop (backtest.py:133-219) run in lock step on the
     device: at every step one batched window launch (kmpc_window over the P
     paths) and one bookkeeping launch (kmpc_backtest_step); calculate_metrics per path at the end
@@ -219,12 +219,15 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
         realized: [P, T, N] float32 de-standardized log-returns (the reference's all_returns).
         mean, std: [N] de-standardisation of the rollout (env.stats).
         n_rows: len(env.test_dataset) (default T); n_steps = n_rows - config.horizon.
+        graph: capture the whole step sequence in one HIP graph and replay it (no per-launch host
+            overhead or inter-kernel gaps: the latency-bound small-P case); same launches, same
+            results as the eager loop.
     Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
         reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
     """
     km = strategy.device_model()
     dev = km.device
-    x = torch.as_tensor(obs).to(dev, torch.float32).contiguous()
+    x = torch.as_tensor(obs).to(dev, torch.float32)
     r = torch.as_tensor(realized).to(dev, torch.float32).contiguous()
     if x.dim() != 3 or r.dim() != 3 or x.shape[:2] != r.shape[:2]:
         raise ValueError("obs must be [P, T, obs] and realized [P, T, N]")
@@ -232,23 +235,38 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
     n_rows = T if n_rows is None else int(n_rows)
     steps = list(range(0, n_rows - config.horizon, config.rebalance_freq))
     S = len(steps)
+    # per step the [P, obs] rows of test index t, contiguous ([T, P, obs]: one copy up front instead
+    # of one gather per step), and the realized returns of t + 1
+    xt = x.transpose(0, 1).contiguous()
+    rt = r.transpose(0, 1).contiguous()
+    m, sd = km._stats(mean, std, N)
     w = torch.full((P, N), 1.0 / N, dtype=torch.float64, device=dev)       # backtest.py:161
     value = torch.full((P,), float(config.initial_capital), dtype=torch.float64, device=dev)
     hist = torch.empty((P, max(S, 1), 4), dtype=torch.float64, device=dev)
     metrics = torch.empty((P, 5), dtype=torch.float64, device=dev)
     L = _lib.load()
     d = _lib.BacktestDesc(P, N, max(S, 1), float(config.cost_coeff))
-    for k, t in enumerate(steps):
-        W0, _, _ = km.window(x[:, t], w, mean, std, N, strategy.mpc_config)
-        rn = r[:, t + 1].contiguous() if t + 1 < T else None
-        with torch.cuda.device(dev):
+
+    def run_steps():
+        for k, t in enumerate(steps):
+            W0, _, _ = km.window(xt[t], w, m, sd, N, strategy.mpc_config)
+            rn = rt[t + 1] if t + 1 < T else None
             _lib.check(L.kmpc_backtest_step(ctypes.byref(d), k, W0.data_ptr(),
                                             rn.data_ptr() if rn is not None else None, w.data_ptr(),
                                             value.data_ptr(), hist.data_ptr(), _lib.stream_handle(dev)))
-    if S:
-        with torch.cuda.device(dev):
+        if S:
             _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), metrics.data_ptr(),
                                                _lib.stream_handle(dev)))
+
+    with torch.cuda.device(dev):
+        if graph and S:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                run_steps()
+            g.replay()
+            torch.cuda.current_stream(dev).synchronize()   # (before the graph and its pool go)
+        else:
+            run_steps()
     hist = hist[:, :S]
     return {"portfolio_value": hist[..., 0], "return": hist[..., 1], "turnover": hist[..., 2],
             "cost": hist[..., 3], "weights": w,

@@ -895,6 +895,11 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
             return KMPC_ERR_LAUNCH;
     }
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
+    // znparts > 0: the last encoder layer left z0 UNWRITTEN — its raw split-K partials sit in
+    // `part`, and the fused latent loop below rebuilds z0 from them (same slice order and bias).
+    // Nothing may be launched between here and that loop that reuses `part` or reads z0
+    // (tests/test_rollout_gpu.py::test_fused_z0_is_never_read fills the workspace with NaN).
+    if (znparts > 0 && !latent_fusable(d)) return KMPC_ERR_INVALID;   // (zfuse implies fusable)
 
     // ---- H x (step_latent, decode[:N], destandardize) ----
     if (latent_fusable(d)) {

@@ -45,6 +45,12 @@ __device__ __forceinline__ int wsumi(int v) {
 }
 constexpr int SIMPLEX_WAVES = 4;   // waves per 256-thread block
 constexpr int SIMPLEX_HR = 16;     // register fast path: N <= 64 assets, H <= 16 periods
+// float32 -> float64 handoff of the mixed-precision pair. Measured on the oracle's iteration
+// (tools/f32phase_probe.py, 512 C3 windows of the bench's distribution: float32 to mu <= 1e-4 takes
+// 7.1 of the 15.8 iterations, every window optimal, float64 finish 8.7 iterations; 2e-5 left 1% of
+// the windows optimal_inaccurate) and on MI355X (tools/mixed_probe.py, 65,536 windows: 1e-4 and
+// 5e-5 within 1% of each other; 5e-5 left 5 random-yhat windows for the retry pass, 1e-4 none)
+constexpr double MU_HANDOFF = 1e-4;
 
 // butterflies within aligned groups of G lanes (G = 32 or 64)
 template <int G>
@@ -238,7 +244,24 @@ SolveArgs make_args(const kmpc_solve_desc* d) {
     a.return_full = d->return_full_W;
     a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 3);
     a.path = d->path;
+    a.warm = nullptr;
+    a.mu_handoff = d->mu_handoff > 0.0 ? d->mu_handoff : MU_HANDOFF;
     return a;
+}
+
+// Mixed precision (kmpc_solve_kernel.h, PH = 1 / 2): the shapes with a float32 / float64 kernel
+// pair — the C3 kernel's (H = 10, 128 threads with N < 104, no short, c > 0 or tau > 0, cap).
+// Windows go through in chunks of at most WARM_CHUNK, one warm record each.
+constexpr int WARM_CHUNK = 131072;
+bool mixed_case(const SolveArgs& a, const kmpc_solve_desc* d) {
+    if (d->precision != KMPC_PRECISION_AUTO) return false;
+    if (a.path != KMPC_PATH_AUTO && a.path != KMPC_PATH_REGISTER && a.path != KMPC_PATH_REGISTER_UNPACKED) return false;
+    const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
+    return fl7 && a.H == 10 && a.N > 64 && a.N < 104;
+}
+size_t warm_bytes(const SolveArgs& a) {
+    const size_t chunk = a.B < WARM_CHUNK ? (size_t)a.B : (size_t)WARM_CHUNK;
+    return sizeof(float) * warm_stride(a.H, a.N) * chunk;
 }
 
 bool use_big(const SolveArgs& a) {
@@ -263,6 +286,7 @@ size_t solve_workspace_bytes(const kmpc_solve_desc* d) {
 #ifndef KMPC_DEV_ONLY_H10
     if (use_big(a)) return big_ws_bytes(a);
 #endif
+    if (mixed_case(a, d)) return warm_bytes(a);
     return 0;
 }
 
@@ -289,6 +313,26 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
                                 : (a.H <= 5 ? launch_ipm_packed<5>(a, stream) : launch_ipm_packed<10>(a, stream));
         if (rc != KMPC_ERR_UNSUPPORTED) return rc;
 #endif
+    }
+    // mixed precision (float32 phase + float64 finish), chunk by chunk
+    if (mixed_case(a, d)) {
+        if (!ws || ws_bytes < warm_bytes(a)) return KMPC_ERR_WORKSPACE;
+        SolveArgs c = a;
+        c.warm = (float*)ws;
+        const size_t HN = (size_t)a.H * a.N;
+        for (int b0 = 0; b0 < a.B; b0 += WARM_CHUNK) {
+            c.B = a.B - b0 < WARM_CHUNK ? a.B - b0 : WARM_CHUNK;
+            c.yhat = a.yhat + (size_t)b0 * HN;
+            c.wp = a.wp + (size_t)b0 * a.N;
+            c.wout = a.wout + (size_t)b0 * (a.return_full ? HN : (size_t)a.N);
+            c.status = a.status + b0;
+            c.obj = a.obj + b0;
+            c.iters = a.iters ? a.iters + b0 : nullptr;
+            c.trace = b0 == 0 ? a.trace : nullptr;
+            const int rc = launch_ipm_c3(c, stream);
+            if (rc != KMPC_OK) return rc;
+        }
+        return KMPC_OK;
     }
     // H == 5 / 10 with N <= 128 in the two common constraint cases: constant-case kernels
     if (a.H == 10 || a.H == 5) {

@@ -17,7 +17,18 @@ struct SolveArgs {
     double* obj;
     int* iters;
     double* trace;   // debug: per-iteration (mu, rd, pr, step) of problem 0, or null
+    // mixed precision (kmpc_solve_kernel.h, PH = 1 / 2): one warm record per window, or null
+    float* warm;
+    double mu_handoff;   // the float32 phase hands its iterate over at mu <= mu_handoff
 };
+
+// Warm record of one window: int flag (1 = warm iterate, 0 = cold: start over), int float32
+// iterations, padding to WARM_HEAD floats, then w, s, l1, l2, l3 as [5][H][N] and z4, l4, nu as
+// [3][H] (float32), padded to 64 B.
+constexpr int WARM_HEAD = 16;
+__host__ __device__ inline size_t warm_stride(int H, int N) {
+    return ((size_t)WARM_HEAD + 5 * (size_t)H * N + 3 * (size_t)H + 15) / 16 * 16;
+}
 
 // ipm_kernel launchers, one translation unit per compile-time horizon bound HM (kmpc_solve_h*.hip)
 template <int HM>

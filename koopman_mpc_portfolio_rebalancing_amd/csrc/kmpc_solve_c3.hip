@@ -6,6 +6,13 @@
 
 namespace kmpc {
 int launch_ipm_c3(const SolveArgs& a, hipStream_t stream) {
+    if (a.warm) {   // mixed precision: the float32 phase, then the float64 finish from its iterates
+        int rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 1>(a, 128, stream);
+        if (rc == KMPC_OK) rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 2>(a, 128, stream);
+        // (the retry of warm starts that did not end optimal: most workgroups exit at once)
+        if (rc == KMPC_OK) rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 3>(a, 128, stream);
+        return rc;
+    }
     return launch_one<10, 128, true, 7, QL_CS, true>(a, 128, stream);
 }
 }  // namespace kmpc

@@ -249,8 +249,9 @@ class DeviceKoopman:
         return y
 
     def window(self, obs: torch.Tensor, w_prev: torch.Tensor, mean, std, n_assets: int, mpc_config,
-               keep_yhat: bool = False, return_full: bool = False):
-        """Fused window (kmpc_window): obs [B, obs], w_prev [B, N] -> (W0 or W, status, value[, yhat])."""
+               keep_yhat: bool = False, return_full: bool = False, with_iters: bool = False):
+        """Fused window (kmpc_window): obs [B, obs], w_prev [B, N] -> (W0 or W, status, value[, yhat]
+        [, iters]) — iters [B] int32 interior-point iterations when with_iters."""
         from .mpc import _solve_desc
         _lib.require_gpu(obs)
         x = obs.to(self.device, torch.float32).contiguous()
@@ -272,13 +273,15 @@ class DeviceKoopman:
         W = torch.empty((B, H, n_assets) if return_full else (B, n_assets), dtype=torch.float64, device=self.device)
         status = torch.empty(B, dtype=torch.int32, device=self.device)
         value = torch.empty(B, dtype=torch.float64, device=self.device)
+        iters = torch.empty(B, dtype=torch.int32, device=self.device) if with_iters else None
         with torch.cuda.device(self.device):
             rc = L.kmpc_window(ctypes.byref(rd), ctypes.byref(sd), x.data_ptr(), wp.data_ptr(),
                                y.data_ptr() if y is not None else None, W.data_ptr(), status.data_ptr(),
-                               value.data_ptr(), None, ws.data_ptr(), nbytes,
-                               _lib.stream_handle(self.device))
+                               value.data_ptr(), iters.data_ptr() if iters is not None else None,
+                               ws.data_ptr(), nbytes, _lib.stream_handle(self.device))
         _lib.check(rc)
-        return (W, status, value, y) if keep_yhat else (W, status, value)
+        out = (W, status, value) + ((y,) if keep_yhat else ()) + ((iters,) if with_iters else ())
+        return out
 
 
 def standardize_panel(log_returns, mean, std, device=None) -> torch.Tensor:

@@ -35,6 +35,8 @@ class MPCConfig:
     tol: float = 1e-9
     n_refine: int = 0  # 0 -> kernel default
     solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM, 3 register IPM without lane-group packing
+    precision: str = "auto"  # kmpc_solve_desc.precision: "auto" (float32 warm-start phase + float64 finish where available) or "f64"
+    mu_handoff: float = 0.0  # float32 -> float64 handoff at mu <= mu_handoff (0 -> kernel default 1e-4)
 
 
 def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:
@@ -48,6 +50,11 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     d.return_full_W = int(bool(full))
     d.n_refine = int(getattr(config, "n_refine", 0))
     d.path = int(getattr(config, "solver_path", 0))
+    prec = getattr(config, "precision", "auto")
+    if prec not in ("auto", "f64"):
+        raise ValueError(f"precision must be 'auto' or 'f64' (got {prec!r})")
+    d.precision = _lib.PRECISION_AUTO if prec == "auto" else _lib.PRECISION_F64
+    d.mu_handoff = float(getattr(config, "mu_handoff", 0.0))
     if d.cost_coeff < 0:
         # -c ||dw||_1 with c < 0 is not concave: the reference's cvxpy problem fails DCP and raises
         raise ValueError(f"cost_coeff must be >= 0 (got {config.cost_coeff}): the problem is not convex")
@@ -108,6 +115,33 @@ def solve_mpc_log_utility_batched(
     if with_iters:
         return W, status, value, iters
     return W, status, value
+
+
+def gross_returns(predicted_log_returns: torch.Tensor) -> torch.Tensor:
+    """R = np.exp(yhat) on the float32 yhat (mpc.py:55), bit for bit as numpy evaluates it
+    (kmpc_gross_returns), as a float32 device tensor of the same shape."""
+    y = predicted_log_returns
+    _lib.require_gpu(y)
+    y = y.to(torch.float32).contiguous()
+    R = torch.empty_like(y)
+    L = _lib.load()
+    with torch.cuda.device(y.device):
+        rc = L.kmpc_gross_returns(y.numel(), y.data_ptr(), R.data_ptr(), _lib.stream_handle(y.device))
+    _lib.check(rc)
+    return R
+
+
+def log_utility_value_batched(W: torch.Tensor, current_weights: torch.Tensor,
+                              predicted_log_returns: torch.Tensor, cost_coeff: float) -> torch.Tensor:
+    """problem.value of the reference program (mpc.py:66-103) at given weights: for each window,
+    sum_t log(R_t . w_t) - c sum_t ||w_t - w_{t-1}||_1 (w_{-1} = current_weights), R = np.exp(yhat)
+    in float32, sums in float64. W [B, H, N], current_weights [B, N], yhat [B, H, N] -> [B] float64.
+    Evaluates any W (e.g. a decision taken on another forecast) in the program of `yhat`."""
+    R = gross_returns(predicted_log_returns).double()
+    W = W.to(torch.float64)
+    wp = current_weights.to(device=W.device, dtype=torch.float64)
+    D = torch.diff(torch.cat([wp[:, None, :], W], 1), dim=1)
+    return torch.log((R * W).sum(-1)).sum(-1) - cost_coeff * D.abs().sum((-1, -2))
 
 
 def _default_device() -> torch.device:

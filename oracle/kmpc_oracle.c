@@ -53,6 +53,15 @@ typedef long double real;
 #define RFMAX fmaxl
 #define RFMIN fminl
 #define API(name) name##_ld
+#elif defined(KMPC_REAL_FLOAT)
+/* float32 build: only tools/dev/f32phase.c (the mixed-precision measurement of DESIGN §3.2) */
+typedef float real;
+#define R_(x) x##f
+#define RSQRT sqrtf
+#define RFABS fabsf
+#define RFMAX fmaxf
+#define RFMIN fminf
+#define API(name) name##_f
 #else
 typedef double real;
 #define R_(x) x

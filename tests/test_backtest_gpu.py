@@ -121,3 +121,26 @@ def test_lockstep_paths_match_sequential_and_reference_runs():
         np.testing.assert_allclose(out["return"][p].cpu().numpy(), df["return"].values, rtol=0, atol=3e-7)
         # (a turnover of 1e-12 is solver noise around w_prev: absolute floor 1e-6)
         np.testing.assert_allclose(out["turnover"][p].cpu().numpy(), df["turnover"].values, rtol=1e-6, atol=1e-6)
+
+
+def test_lockstep_graph_replay_equals_eager_loop():
+    """run_backtest_lockstep(graph=True): the whole step sequence (window + bookkeeping launches of
+    every step, then the metrics) captured in one HIP graph and replayed gives the eager loop's
+    histories, weights and metrics bit for bit (C3-shaped model, 64 paths)."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, P, T = 100, 256, 10, 64, 24
+    obs_n = N * 20
+    spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(P, T, obs_n, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    eager = run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    graph = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=True)
+    for k in ("portfolio_value", "return", "turnover", "cost", "weights"):
+        assert torch.equal(eager[k], graph[k]), k
+    for k, v in eager["metrics"].items():
+        assert torch.equal(v, graph["metrics"][k]), k

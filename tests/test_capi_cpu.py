@@ -46,7 +46,18 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d.cost_coeff, d.path = 0.0, 7           # unknown solver path
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
-    d.path = 0
+    d.path, d.precision = 0, 2              # unknown precision
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d.precision, d.mu_handoff = 0, 1.5       # a handoff past mu = 1 is no handoff
+    assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d.mu_handoff = 0.0
+    # the mixed-precision pair (C3 shape) needs one float32 iterate record per window
+    d.B, d.N, d.H, d.cost_coeff, d.max_turnover = 1000, 100, 10, 1e-3, 0.2
+    rec = ((16 + 5 * 10 * 100 + 3 * 10 + 15) // 16) * 16 * 4
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) >= 1000 * rec
+    d.precision = 1
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 0
+    d.B, d.N, d.H, d.cost_coeff, d.max_turnover, d.precision = 0, 5, 5, 0.0, 0.0, 0
     assert lib.kmpc_gross_returns(0, None, None, None) == 0
     assert lib.kmpc_gross_returns(4, None, None, None) == -1
     bt = _lib.BacktestDesc(2, 3, 4, 1e-3)
@@ -72,9 +83,10 @@ def test_struct_layouts_match_header(tmp_path):
 #include <stddef.h>
 #include "{HEADER}"
 int main(void) {{
-  printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_solve_desc), offsetof(kmpc_solve_desc, tol),
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(kmpc_solve_desc), offsetof(kmpc_solve_desc, tol),
          offsetof(kmpc_solve_desc, return_full_W), offsetof(kmpc_solve_desc, max_turnover),
-         offsetof(kmpc_solve_desc, path));
+         offsetof(kmpc_solve_desc, path), offsetof(kmpc_solve_desc, precision),
+         offsetof(kmpc_solve_desc, mu_handoff));
   printf("%zu %zu %zu\\n", sizeof(kmpc_mlp), offsetof(kmpc_mlp, weight), offsetof(kmpc_mlp, bias));
   printf("%zu %zu %zu %zu %zu\\n", sizeof(kmpc_rollout_desc), offsetof(kmpc_rollout_desc, encoder),
          offsetof(kmpc_rollout_desc, lista_thresh), offsetof(kmpc_rollout_desc, decoder),
@@ -92,6 +104,7 @@ int main(void) {{
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     S, M, R, Bt, Mv = _lib.SolveDesc, _lib.Mlp, _lib.RolloutDesc, _lib.BacktestDesc, _lib.MvDesc
     expect = [ctypes.sizeof(S), S.tol.offset, S.return_full_W.offset, S.max_turnover.offset, S.path.offset,
+              S.precision.offset, S.mu_handoff.offset,
               ctypes.sizeof(M), M.weight.offset, M.bias.offset,
               ctypes.sizeof(R), R.encoder.offset, R.lista_thresh.offset, R.decoder.offset, R.std.offset,
               R.obs_ld.offset, R.dtype.offset, R.latent_unfused.offset,

@@ -1,0 +1,136 @@
+"""GPU parity of the mixed-precision solve (kmpc_solve_desc.precision = AUTO at the C3 shape): a
+float32 interior-point phase (ipm_kernel PH = 1) hands its iterate over at mu <= mu_handoff, and the
+float64 kernel (PH = 2) finishes from it under the same stopping and status rules as the float64-only
+solve (precision = F64). The answer's bar is the float64 solve's (test_solver_gpu.py): objective
+within 1e-6 + 1e-5 |f*| of the long-double oracle, W[0] within 1e-3 (c > 0: unique optimum),
+feasibility to 1e-8 — the float32 phase only chooses the starting point of the float64 iteration.
+
+Also BASELINE configs[3]'s per-rank workload (131,072 windows per rank at N = 8) on one
+GPU, and a batch past the 131,072-window chunk of the warm records.
+"""
+import numpy as np
+import pytest
+import torch
+
+from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig, _lib,
+                                                   solve_mpc_log_utility_batched)
+from oracle import solver as oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(wp, y, cfg, full=False):
+    W, st, val, it = solve_mpc_log_utility_batched(torch.as_tensor(wp, device="cuda"), torch.as_tensor(y, device="cuda"),
+                                                   cfg, return_full=full, with_iters=True)
+    return W.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy(), it.cpu().numpy()
+
+
+def _feasible(W, wp, tau, tol=1e-8):
+    D = np.diff(np.concatenate([wp[:, None], W], 1), axis=1)
+    return (np.abs(W.sum(-1) - 1).max() <= tol and W.min() >= -1e-9
+            and np.abs(D).sum(-1).max() <= tau + tol)
+
+
+def test_mixed_equals_f64_at_the_bar_with_cold_windows():
+    """C3 shape, 2,048 windows with a non-finite window (solver_error), an underflowed period
+    (infeasible) and an infeasible cap among them: the float32 phase marks those cold and the
+    float64 kernel reproduces the float64-only statuses and fallbacks; every other window matches
+    the float64-only solve and the oracle at the parity bar."""
+    rng = np.random.default_rng(11)
+    B, N, H = 2048, 100, 10
+    wp = rng.dirichlet(np.ones(N), B)
+    y = rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32)
+    y[5, 3, 7] = np.nan                      # solver_error
+    y[9, H - 1, :] = -110.0                  # every R of a period underflows: infeasible
+    wp[13] = 0.0
+    wp[13, 0] = 3.0                          # sum(w_prev) = 3: the cap makes the budget unreachable
+    c, tau = 1e-3, 0.2
+    Wm, stm, vm, itm = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau), full=True)
+    Wd, std_, vd, itd = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, precision="f64"), full=True)
+    assert np.array_equal(stm, std_)
+    assert stm[5] == 4 and stm[9] == 2 and stm[13] == 2
+    for b in (5, 9, 13):
+        assert np.array_equal(Wm[b], np.tile(wp[b], (H, 1))) and np.isnan(vm[b])
+    ok = np.ones(B, bool)
+    ok[[5, 9, 13]] = False
+    assert (stm[ok] == 0).all()
+    assert np.abs(vm[ok] - vd[ok]).max() <= 1e-6 + 1e-5 * np.abs(vd[ok]).max()
+    assert np.abs(Wm[ok, 0] - Wd[ok, 0]).max() < 1e-3
+    assert _feasible(Wm[ok], wp[ok], tau)
+    # run-to-run bit-identical
+    Wm2, stm2, vm2, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau), full=True)
+    assert np.array_equal(Wm, Wm2) and np.array_equal(vm, vm2, equal_nan=True)
+    # iterations: float32 + float64 ones, about the float64-only count (tools/f32phase_probe.py)
+    assert abs(itm[ok].mean() - itd[ok].mean()) < 2.0
+    idx = np.concatenate([np.arange(0, 48), [5, 9, 13], np.arange(B - 16, B)])
+    Wo, sto, valo, _ = oracle.solve_batch(wp[idx], y[idx], c, tau)
+    assert np.array_equal(stm[idx] <= 1, sto <= 1)
+    k = sto <= 1
+    assert np.abs(vm[idx][k] - valo[k]).max() <= 1e-6 + 1e-5 * np.abs(valo[k]).max()
+    assert np.abs(Wm[idx][k, 0] - Wo[k, 0]).max() < 1e-3
+
+
+@pytest.mark.parametrize("mu_handoff", [1e-3, 1e-4, 2e-5])
+def test_mixed_handoff_threshold_keeps_parity(mu_handoff):
+    """Earlier and later handoffs (MPCConfig.mu_handoff) change only the float64 start."""
+    rng = np.random.default_rng(int(1 / mu_handoff))
+    B, N, H = 256, 90, 10
+    wp = rng.dirichlet(np.ones(N), B)
+    y = rng.normal(5e-4, 0.02, (B, H, N)).astype(np.float32)
+    W, st, val, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=2e-3, max_turnover=0.3, mu_handoff=mu_handoff))
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y, 2e-3, 0.3)
+    assert (sto == 0).all() and (st <= 1).all()
+    assert np.abs(val - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
+    assert np.abs(W - Wo[:, 0]).max() < 1e-3
+
+
+def test_warm_records_chunk_boundary():
+    """Past 131,072 windows the warm records are reused chunk by chunk: windows on either side of
+    the boundary equal the same windows solved alone, bit for bit."""
+    rng = np.random.default_rng(3)
+    B, N, H = 131072 + 96, 100, 10
+    wp = rng.dirichlet(np.ones(N), B)
+    y = rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    W, st, val, it = _solve(wp, y, cfg)
+    assert (st == 0).all()
+    lo = 131072 - 32
+    W1, st1, val1, it1 = _solve(wp[lo:], y[lo:], cfg)
+    assert np.array_equal(W1, W[lo:]) and np.array_equal(val1, val[lo:]) and np.array_equal(it1, it[lo:])
+
+
+def test_config3_per_rank_workload_on_one_gpu():
+    """BASELINE configs[3] at N = 8 gives each rank 131,072 windows. The headline model
+    (finance_sparse GenericKM, obs 2000, latent 256) over that many windows of the bench's own stream
+    (rank 0's block), fused window path: every window optimal and feasible, never worse than holding
+    w_prev, and the first and last 64 windows against the long-double oracle on the device's yhat."""
+    import bench
+    dev = torch.device("cuda")
+    B, N, L, H = 131072, 100, 256, 10
+    obs_n = N * 20
+    sd = bench.make_state_dict(obs_n, L, 1024, seed=0)
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), dev)
+    x, wp = bench.window_inputs(0, B, N, obs_n, seed=0, device=dev)
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    W0, st, val, y = km.window(x, wp, mean, std, N, cfg, keep_yhat=True)
+    st = st.cpu().numpy()
+    assert (st == 0).all()
+    W0n, wpn, valn = W0.cpu().numpy(), wp.cpu().numpy(), val.cpu().numpy()
+    assert np.abs(W0n.sum(-1) - 1).max() < 1e-8 and W0n.min() > -1e-9
+    assert np.abs(W0n - wpn).sum(-1).max() <= 0.2 + 1e-8
+    R = _lib_gross(y)
+    hold = np.log(np.einsum("bhn,bn->bh", R, wpn)).sum(-1)
+    assert (valn >= hold - 1e-9).all()
+    idx = np.concatenate([np.arange(64), np.arange(B - 64, B)])
+    yn = y[idx].cpu().numpy()
+    Wo, sto, valo, _ = oracle.solve_batch(wpn[idx], yn, 1e-3, 0.2)
+    assert (sto == 0).all()
+    assert np.abs(valn[idx] - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
+    assert np.abs(W0n[idx] - Wo[:, 0]).max() < 1e-3
+
+
+def _lib_gross(y):
+    from koopman_mpc_portfolio_rebalancing_amd import gross_returns
+    return gross_returns(y).double().cpu().numpy()

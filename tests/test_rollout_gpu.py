@@ -289,3 +289,34 @@ def test_encoder_gemm_tiles_match_numpy(B):
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
     dec = ref - mean
     assert_rel(y - ref, np.abs(dec).max(), 1e-5, f"encoder tiles B{B}")
+
+
+def test_fused_z0_is_never_read():
+    """configs[1] shape (4,096 windows, N = 30, latent 128, encoder [1024, 1024]): the last encoder
+    layer runs split-K and leaves z0 unwritten; the fused latent loop rebuilds z0 from the raw
+    partials (kmpc_rollout.hip, znparts). With the whole workspace pre-filled with NaN, yhat must
+    be finite and bit-identical to a zero-filled workspace — nothing reads z0 (or a stale part)."""
+    import ctypes
+    import bench
+    from koopman_mpc_portfolio_rebalancing_amd import _lib
+    dev = torch.device("cuda")
+    B, N, L, H = 4096, 30, 128, 5
+    obs_n = N * 20
+    km = DeviceKoopman(KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=1),
+                                                        bench.MODEL_CFG), dev)
+    x, _ = bench.window_inputs(0, B, N, obs_n, seed=1, device=dev)
+    m = torch.full((N,), 5e-4, device=dev)
+    s = torch.full((N,), 0.015, device=dev)
+    d = km.rollout_desc(B, H, N, m, s)
+    Lb = _lib.load()
+    nbytes = Lb.kmpc_workspace_bytes(ctypes.byref(d), None)
+    outs = []
+    for fill in (0xFF, 0x00):   # 0xFFFFFFFF is a float32 NaN
+        ws = torch.full((nbytes,), fill, dtype=torch.uint8, device=dev)
+        y = torch.empty((B, H, N), dtype=torch.float32, device=dev)
+        _lib.check(Lb.kmpc_rollout(ctypes.byref(d), x.data_ptr(), y.data_ptr(), ws.data_ptr(), nbytes,
+                                   _lib.stream_handle(dev)))
+        outs.append(y)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], km.rollout(x, m, s, H, N))

@@ -21,12 +21,13 @@ for P, T in ((64, 260), (1024, 260), (8192, 60)):
     r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
     cfg = BacktestConfig(horizon=H)
     mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
-    out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std)   # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out = run_backtest_lockstep(strat, x, r, cfg, mean, std)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    S = out["return"].shape[1]
-    print(f"P={P} T={T}: {S} steps in {dt*1e3:.1f} ms -> {P*S/dt:.0f} path-steps/s, {dt/S*1e3:.3f} ms/step, "
-          f"final value mean {out['portfolio_value'][:, -1].mean().item():.1f}", flush=True)
+    for graph in (False, True):
+        out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std, graph=graph)   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=graph)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        S = out["return"].shape[1]
+        print(f"P={P} T={T} graph={graph}: {S} steps in {dt*1e3:.1f} ms -> {P*S/dt:.0f} path-steps/s, "
+              f"{dt/S*1e3:.3f} ms/step, final value mean {out['portfolio_value'][:, -1].mean().item():.1f}", flush=True)

@@ -1,0 +1,59 @@
+"""Dev probe (GPU): the mixed-precision C3 solve (float32 warm-start phase + float64 finish) against
+the float64-only solve, on the bench's own yhat (GPU rollout of the bench model over
+window_inputs(0, B)) and on random yhat ~ N(5e-4, 0.015). Per handoff threshold: time per launch,
+mean iterations, statuses, max |obj - obj_f64| and max |W0 - W0_f64|.
+
+    python tools/mixed_probe.py [B] [mu_handoff,...]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+import bench
+from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig, _lib,
+                                                   solve_mpc_log_utility_batched)
+if os.environ.get("KMPC_DEV_LIB"):   # a variant library built by csrc/Makefile (tvar / var)
+    _lib._lib = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["KMPC_DEV_LIB"]))
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+MUS = [float(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1e-4,5e-5,2e-5").split(",")]
+REPS = int(os.environ.get("REPS", "3"))
+dev = torch.device("cuda", 0)
+N, L, H = 100, 256, 10
+obs = N * 20
+sd = bench.make_state_dict(obs, L, 1024, seed=0)
+model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), dev)
+x, wp = bench.window_inputs(0, B, N, obs, seed=0, device=dev)
+mean_d = torch.full((N,), 5e-4, device=dev)
+std_d = torch.full((N,), 0.015, device=dev)
+y_bench = model.rollout(x, mean_d, std_d, H, N)
+rng = np.random.default_rng(0)
+y_rand = torch.tensor(rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32), device=dev)
+
+
+def run(y, cfg):
+    best = 1e30
+    for _ in range(REPS):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        W, s, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    return best, W, s, v, it
+
+
+for name, y in (("bench", y_bench), ("random", y_rand)):
+    dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64"))
+    print(f"[{name}] f64: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters {it64.float().mean().item():.2f} "
+          f"status {np.bincount(s64.cpu().numpy(), minlength=5)}", flush=True)
+    for mu in MUS:
+        dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu))
+        ok = (s <= 1) & (s64 <= 1)
+        print(f"[{name}] mixed mu_handoff={mu:g}: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters "
+              f"{it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)} "
+              f"max|dobj| {(v - v64)[ok].abs().max().item():.3e} max|dW0| {(W - W64)[ok].abs().max().item():.3e} "
+              f"status==f64 {int((s == s64).sum().item())}/{B}", flush=True)
