@@ -536,6 +536,8 @@ def secondary_c5(dev, steps: int, warmup: int, B: int = 1024) -> dict:
             "rollout_ms": roll / k, "solve_ms": solv / k,
             "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B,
             "fp32_rollout_ms": r32 / k,
+            # the default (fp32) rollout's configs[4] rate from the same kernel timings
+            "windows_per_s_fp32_rollout_kernels": B / ((r32 + solv) / k * 1e-3),
             "bf16_decision_gap": {"max": float(gap.max()), "p99": float(np.percentile(gap, 99)),
                                   "median": float(np.median(gap)), "windows": int(gap.size),
                                   "windows_over_objective_bar": int((gap > bar).sum()),

@@ -42,11 +42,15 @@ constexpr int WAVE = 64;
 #ifdef KMPC_STATS
 __device__ unsigned long long g_stats[2];   // dev builds only: refinement steps, Newton solves
 __device__ unsigned long long g_phase[16];  // dev builds only: s_memtime cycles per solver phase
+// KMPC_STATS_REAL = 4 / 8: count only the float32 / float64 kernels of a translation unit
+#ifndef KMPC_STATS_REAL
+#define KMPC_STATS_REAL 0
+#endif
 struct PhaseClock {
     unsigned long long last;
     bool on;
-    __device__ __forceinline__ void start() {
-        on = threadIdx.x == 0 && (blockIdx.x & 255) == 0;
+    __device__ __forceinline__ void start(int real_bytes) {
+        on = threadIdx.x == 0 && (blockIdx.x & 255) == 0 && (KMPC_STATS_REAL == 0 || real_bytes == KMPC_STATS_REAL);
         last = __builtin_amdgcn_s_memtime();
     }
     __device__ __forceinline__ void mark(int k) {
@@ -55,7 +59,7 @@ struct PhaseClock {
         last = now;
     }
 };
-#define KMPC_PH_START(P) P.start()
+#define KMPC_PH_START(P) P.start((int)sizeof(Real))
 #define KMPC_PH(P, k) P.mark(k)
 // dev builds only (tools/phase_stats.py): out[0..1] = refinement steps, Newton solves;
 // out[2..17] = s_memtime cycles per solver phase. reset != 0 zeroes the counters afterwards.
@@ -84,9 +88,16 @@ struct PhaseClock {};
 #ifndef KMPC_WPE2_HM
 #define KMPC_WPE2_HM 5
 #endif
-// waves per SIMD of the float32 warm-start phase (PH = 1): its state takes half the registers
+// waves per SIMD of the float32 warm-start phase (PH = 1). At one wave per SIMD its whole state,
+// cold arrays included, fits the registers without spills (424 of 512): measured against two waves
+// per SIMD with the cold arrays in LDS (87 spilled VGPRs) — C3 mixed solve 85.8 -> 83.5 ms
+// (tools/ab_mixed.sh); two waves per SIMD without the LDS change: no difference
 #ifndef KMPC_F32_WPE
-#define KMPC_F32_WPE 2
+#define KMPC_F32_WPE 1
+#endif
+// dev A/B: park w, s in scratch across the float32 phase's Newton solves as the float64 kernel does
+#ifndef KMPC_F32_PARK
+#define KMPC_F32_PARK 0
 #endif
 #ifndef KMPC_REFINE_RTOL
 #define KMPC_REFINE_RTOL 1e-7
@@ -522,10 +533,9 @@ __host__ __device__ constexpr int n_cold(bool ql) { return ql ? 8 : 6; }
 #ifndef KMPC_PACKED_COLD_REG   // dev A/B: every packed kernel's cold arrays in registers
 #define KMPC_PACKED_COLD_REG 0
 #endif
-// dev A/B: the float32 phase's cold arrays in registers (it has ~150 registers to spare at one
-// wave per SIMD)
+// the float32 phase keeps its cold arrays in registers (KMPC_F32_WPE above; 0 = in LDS, dev A/B)
 #ifndef KMPC_F32_COLD_REG
-#define KMPC_F32_COLD_REG 0
+#define KMPC_F32_COLD_REG 1
 #endif
 template <int HM, int MAXT, int CS, bool QL, int GL = 64, int FL = -1, class Real = double>
 constexpr bool cold_in_lds() {
@@ -1216,7 +1226,7 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM, typename TH::real_
             pxa += pv;
         }
 #ifdef KMPC_STATS
-        if (threadIdx.x == 0 && (blockIdx.x & 255) == 0) atomicAdd(&g_phase[7], __builtin_amdgcn_s_memtime() - t_ls);
+        if (np.on) atomicAdd(&g_phase[7], __builtin_amdgcn_s_memtime() - t_ls);
 #endif
         if (r == 0) {
 #pragma unroll
@@ -1272,7 +1282,10 @@ __device__ __forceinline__ void newton(TH& T, Shared<HM, NWM, typename TH::real_
         __syncthreads();
     }
 #ifdef KMPC_STATS
-    if (threadIdx.x == 0) { atomicAdd(&g_stats[0], (unsigned long long)r); atomicAdd(&g_stats[1], 1ull); }
+    if (threadIdx.x == 0 && (KMPC_STATS_REAL == 0 || sizeof(Real) == KMPC_STATS_REAL)) {
+        atomicAdd(&g_stats[0], (unsigned long long)r);
+        atomicAdd(&g_stats[1], 1ull);
+    }
 #endif
     // dz4 / dl4 of the final direction on the period owners: sum_i ds_t = sum_i P (bs - rho px) =
     // px (1 - rho SP) = px / (1 + gamma SP) summed over the passes — no reduction, and no barrier:
@@ -1980,13 +1993,16 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
                     // reloads it piecemeal inside the iteration (107 -> 54 spilled dwords; C3 solve
                     // +6%, N = 250 +16%, measured r02). The empty asm takes the array's address,
                     // so it stays in memory and the loads are not forwarded from the stores.
+                    // (the float32 phase has registers to spare at one wave per SIMD: no parking
+                    // unless KMPC_F32_PARK)
+                    constexpr bool PARK = sizeof(Real) == 8 || KMPC_F32_PARK;
                     Real park[2 * HM];
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { park[t] = T.w[t]; park[HM + t] = T.s[t]; }
-                    asm volatile("" :: "v"(&park[0]) : "memory");
+                    if constexpr (PARK) asm volatile("" :: "v"(&park[0]) : "memory");
                     newton<HM, NWM>(T, sh, R, (PH == 1 || pass == 0 || mu > (T.hw ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : args.n_refine,
                                     pass == 0);
-                    asm volatile("" :: "v"(&park[0]) : "memory");
+                    if constexpr (PARK) asm volatile("" :: "v"(&park[0]) : "memory");
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { T.w[t] = park[t]; T.s[t] = park[HM + t]; }
                     KMPC_PH(ph, 4);

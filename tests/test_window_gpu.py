@@ -158,3 +158,48 @@ def test_config0_model_rollout_and_window():
     assert (st.cpu().numpy() == 0).all()
     _check_against_oracle(W0.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy(), wp.cpu().numpy(), yn, cfg,
                           np.arange(0, B, 97))
+
+
+def test_config5_bf16_decision_gap_in_fp32_program():
+    """VERDICT r04 item 1 — decision-level parity of the bf16 rollout. The reference rolls out in
+    fp32 (/root/reference/model.py:828-850) and solves on that yhat (mpc.py:55-104); BASELINE
+    configs[4] asks for a bf16 MFMA rollout. The bf16 path's decision W^bf16 (the full [H, N] plan)
+    is evaluated in the program of the fp32 yhat: gap = f*(fp32) - f(W^bf16; fp32 yhat) in
+    problem.value units, with f* at the fp32 solve's own W (optimal at the solver's bar).
+
+    Measured (bench.secondary_c5, 1,024 windows): max 1.7e-5, p99 1.0e-5, median 4.5e-7 — above the
+    objective bar 1e-6 + 1e-5 |f*| on 23% of the windows. So the fp32 rollout is the default of
+    DeviceKoopman and of the strategy path at that shape (it costs +0.6 ms of a 66 ms step), and
+    bf16 is the opt-in configuration BASELINE names, reported with this gap. Bound asserted here:
+    gap <= 5e-5 (3x the measured maximum), and never below -bar (the fp32 decision is optimal)."""
+    import bench
+    from koopman_mpc_portfolio_rebalancing_amd import log_utility_value_batched
+    dev = torch.device("cuda")
+    N, L, H, B = 500, 512, 20, 640
+    obs_n = N * 20
+    sd, lc = bench.make_lista_state_dict(obs_n, L, seed=2)
+    cfg_m = {"MODEL": {"MODEL_NAME": "LISTAKM", "NORM_FN": "id",
+                       "ENCODER": {"LISTA": {"ALPHA": 5e-3, "L": lc, "NUM_LOOPS": 10}}}}
+    spec = KoopmanModelSpec.from_state_dict(sd, cfg_m)
+    km16 = DeviceKoopman(spec, dev, dtype="bf16")
+    km32 = DeviceKoopman(spec, dev)
+    assert km32.dtype == "fp32"
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    assert KoopmanMPCStrategy(spec, cfg).device_model().dtype == "fp32"
+    x, wp = bench.window_inputs(0, B, N, obs_n, seed=8, device=dev)
+    mean = torch.full((N,), 5e-4, device=dev)
+    std = torch.full((N,), 0.015, device=dev)
+    y32 = km32.rollout(x, mean, std, H, N)
+    y16 = km16.rollout(x, mean, std, H, N)
+    W32, st32, v32 = solve_mpc_log_utility_batched(wp, y32, cfg, return_full=True)
+    W16, st16, _ = solve_mpc_log_utility_batched(wp, y16, cfg, return_full=True)
+    assert (st32 == 0).all() and (st16 == 0).all()
+    f32 = log_utility_value_batched(W32, wp, y32, cfg.cost_coeff)
+    f16 = log_utility_value_batched(W16, wp, y32, cfg.cost_coeff)
+    assert torch.allclose(f32, v32, rtol=0, atol=1e-12)       # the kernel's value is problem.value at W32
+    gap = (f32 - f16).cpu().numpy()
+    bar = (1e-6 + 1e-5 * f32.abs()).cpu().numpy()
+    print(f"[bf16 gap] max {gap.max():.3e} p99 {np.percentile(gap, 99):.3e} median {np.median(gap):.3e} "
+          f"over bar {(gap > bar).mean():.2%}")
+    assert (gap >= -bar).all()
+    assert gap.max() <= 5e-5

@@ -15,13 +15,14 @@ N, L, H = 100, 256, 10
 obs = N * 20
 spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs, L, 1024, seed=0), bench.MODEL_CFG)
 strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
-for P, T in ((64, 260), (1024, 260), (8192, 60)):
+CASES = [tuple(int(v) for v in c.split('x')) for c in os.environ.get('CASES', '64x260,1024x260,8192x60').split(',')]
+for P, T in CASES:
     g = torch.Generator().manual_seed(0)
     x = torch.randn(P, T, obs, generator=g).to(dev)
     r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
     cfg = BacktestConfig(horizon=H)
     mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
-    for graph in (False, True):
+    for graph in [g_ == '1' for g_ in os.environ.get('GRAPH', '0,1').split(',')]:
         out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std, graph=graph)   # warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -39,7 +39,7 @@ libs = sys.argv[2:] or sorted(os.path.basename(p) for p in glob.glob(os.path.joi
 for name in libs:
     L = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), name))
     _lib._lib = L
-    cfg = MPCConfig(horizon=H)
+    cfg = MPCConfig(horizon=H, precision=os.environ.get("PRECISION", "auto"))
     solve_mpc_log_utility_batched(wp, y, cfg); torch.cuda.synchronize()
     read_stats(L)
     t = time.time()
@@ -54,4 +54,4 @@ for name in libs:
           f"dW0 {np.abs(W[:nchk].cpu().numpy() - Wo[:, 0]).max():.2e}")
     for k in range(16):
         c = st[2 + k] / nb / iters
-        print(f"   {names[k]:14s} {c:10.0f} cycles/iter  {100*st[2+k]/max(tot,1):5.1f}%")
+        print(f"   {names[k]:14s} {c:10.0f} cycles/iter  {st[2 + k] / nb:12.0f} cycles/window  {100*st[2+k]/max(tot,1):5.1f}%")
