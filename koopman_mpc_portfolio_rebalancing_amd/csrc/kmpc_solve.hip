@@ -46,11 +46,11 @@ __device__ __forceinline__ int wsumi(int v) {
 constexpr int SIMPLEX_WAVES = 4;   // waves per 256-thread block
 constexpr int SIMPLEX_HR = 16;     // register fast path: N <= 64 assets, H <= 16 periods
 // float32 -> float64 handoff of the mixed-precision pair. Measured on the oracle's iteration
-// (tools/f32phase_probe.py, 512 C3 windows of the bench's distribution: float32 to mu <= 1e-4 takes
-// 7.1 of the 15.8 iterations, every window optimal, float64 finish 8.7 iterations; 2e-5 left 1% of
-// the windows optimal_inaccurate) and on MI355X (tools/mixed_probe.py, 65,536 windows: 1e-4 and
-// 5e-5 within 1% of each other; 5e-5 left 5 random-yhat windows for the retry pass, 1e-4 none)
-constexpr double MU_HANDOFF = 1e-4;
+// (tools/f32phase_probe.py, 512 C3 windows of the bench's distribution: float32 to mu <= 5e-5 takes
+// 7.9 of the 15.9 iterations, every window optimal, float64 finish 8.0 iterations; 2e-5 left 1% of
+// the windows optimal_inaccurate) and on MI355X (tools/ab_mixed.sh, 65,536 windows, retry pass in:
+// bench yhat 83.3 ms at 1e-4, 82.0 ms at 5e-5; random yhat 91.1 / 90.7 ms, same statuses as float64)
+constexpr double MU_HANDOFF = 5e-5;
 
 // butterflies within aligned groups of G lanes (G = 32 or 64)
 template <int G>

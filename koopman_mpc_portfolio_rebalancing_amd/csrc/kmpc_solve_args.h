@@ -22,6 +22,10 @@ struct SolveArgs {
     double mu_handoff;   // the float32 phase hands its iterate over at mu <= mu_handoff
 };
 
+// A period whose gross returns R = np.exp(yhat) sum below this is solved on R / sum(R) (the same
+// program up to the constant log sum(R); 1 + m = R would lose R's digits): every kernel and the oracle
+constexpr double TINY_PERIOD = 0x1p-16;
+
 // Warm record of one window: int flag (1 = warm iterate, 0 = cold: start over), int float32
 // iterations, padding to WARM_HEAD floats, then w, s, l1, l2, l3 as [5][H][N] and z4, l4, nu as
 // [3][H] (float32), padded to 64 B.

@@ -98,6 +98,7 @@ struct BigShared {
     double rw[HM], best_rw[HM], best_l1[HM], px[HM], adw[HM], sds[HM], sdw[HM];
     double isp1[HM];   // 1 / (1 + gamma SP), SP = sum_i P (rho = gamma isp1)
     double pxa[HM];    // the direction's px summed over its solves: ds = P (DS - rho pxa), sum_i ds = pxa isp1
+    double lsc[HM];    // log S_t of a period run on R / S_t (tiny gross returns), else 0
     int flag;
 };
 
@@ -167,6 +168,10 @@ struct Win {
     __device__ __forceinline__ double mload(int t) const {
         const unsigned so = (unsigned)(A_M * HM * NP) * 8u + (unsigned)(t * NP) * 4u;
         return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo >> 1, so, 0)) - 1.0;
+    }
+    __device__ __forceinline__ double rload(int t) const {   // the stored float32 R itself
+        const unsigned so = (unsigned)(A_M * HM * NP) * 8u + (unsigned)(t * NP) * 4u;
+        return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo >> 1, so, 0));
     }
     __device__ __forceinline__ void mstore(int t, float r) const {
         const unsigned so = (unsigned)(A_M * HM * NP) * 8u + (unsigned)(t * NP) * 4u;
@@ -1359,24 +1364,36 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
             if (!isfinite(W.wpi)) nf = 1.0;
             for (int t = 0; t < H; ++t) {
                 const float r = np_expf(yh[t * N + i]);
-                const double m = (double)r - 1.0;
-                if (!isfinite(m)) nf = 1.0;
+                if (!isfinite((double)r - 1.0)) nf = 1.0;
                 W.mstore(t, r);
-                mx = fmax(mx, fabs(m));
+            }
+        }
+        {
+            double z = 0.0;
+            W.sum_max(z, nf);
+        }
+        // per period S_t = sum_i R: 0 -> the reference's exp cone is infeasible; below TINY_PERIOD the
+        // period runs on R / S_t (stored back as float32) and the objective adds log S_t (as
+        // ipm_kernel and the oracle)
+        bool r_zero = false;
+        if (nf == 0.0) {
+            for (int t = 0; t < H; ++t) W.slot(t, W.act ? W.rload(t) : 0.0);
+            W.finish(H);
+            for (int t = 0; t < H; ++t) {
+                const double S = sh.tot[t];
+                r_zero = r_zero || S == 0.0;
+                if (S > 0.0 && S < TINY_PERIOD && W.act) W.mstore(t, (float)(W.rload(t) / S));
+                if (W.act) mx = fmax(mx, fabs(W.mload(t)));
+            }
+            if (threadIdx.x < HM) {
+                const int t = threadIdx.x;
+                const double S = t < H ? sh.tot[t] : 1.0;
+                sh.lsc[t] = (S > 0.0 && S < TINY_PERIOD) ? log(S) : 0.0;
             }
         }
         {
             double z = 0.0;
             W.sum_max(z, mx);
-            z = 0.0;
-            W.sum_max(z, nf);
-        }
-        // a period whose every R is 0: the reference's exp cone is infeasible (as ipm_kernel)
-        bool r_zero = false;
-        if (nf == 0.0) {
-            for (int t = 0; t < H; ++t) W.slot(t, W.act ? 1.0 + W.mload(t) : 0.0);
-            W.finish(H);
-            for (int t = 0; t < H; ++t) r_zero = r_zero || sh.tot[t] == 0.0;
         }
         double sig = fmax(mx, a.c);
         if (!(sig > 0.0)) sig = 1.0;
@@ -1407,7 +1424,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                     }
                     W.finish(H);
                     double f = 0.0;
-                    for (int t = 0; t < H; ++t) f += log(sh.tot[t]);
+                    for (int t = 0; t < H; ++t) f += log(sh.tot[t]) + sh.lsc[t];
                     best_obj = f;
                     status = KMPC_STATUS_OPTIMAL;
                 } else {
@@ -1445,7 +1462,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                 __syncthreads();   // sh.best_* of the best iterate visible
                 if (best < 1e300) {
                     double f = 0.0;
-                    for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) - a.c * sh.best_l1[t];
+                    for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) + sh.lsc[t] - a.c * sh.best_l1[t];
                     best_obj = f;
                 }
                 if (best <= 1e-7) status = KMPC_STATUS_OPTIMAL;

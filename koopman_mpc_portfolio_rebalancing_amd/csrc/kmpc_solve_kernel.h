@@ -572,6 +572,7 @@ struct Shared {
     Real pxd[NWM][pow2_at_least(HM)];  // (read only by an untaken branch of lsolve: see there)
     Real rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     Real best_rw[HM], best_l1[HM];   // per-period R.w and ||w_t - w_{t-1}||_1 of the best iterate
+    Real lsc[HM];                    // log S_t of a period run on R / S_t (tiny gross returns), else 0
     int flag;
 };
 
@@ -1701,7 +1702,7 @@ __device__ __forceinline__ Real record_best(const TH& T, Reducer<HM, NWM, TH::GL
     Real f = Real(0.0);
 #pragma unroll
     for (int t = 0; t < HM; ++t)
-        if (t < H) f += log(rw[t]) - c * l1n[t];
+        if (t < H) f += log(rw[t]) + R.sh.lsc[t] - c * l1n[t];   // (+ log S_t of a rescaled period)
     return f;
 }
 
@@ -1720,6 +1721,12 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
     using Real = std::conditional_t<PH == 1, float, double>;
     constexpr int NWM = MAXT / WAVE;
     constexpr int WPB = GL == 64 ? 1 : 64 / GL;   // windows per block
+    // cold_in_lds() sizes the static LDS with a fixed estimate (9 HM^2 doubles + 16 KB): it must
+    // cover the real Shared, and static + dynamic LDS must fit one CU
+    static_assert(!cold_in_lds<HM, MAXT, CS, QL, GL, FL, Real>() ||
+                  sizeof(Shared<HM, NWM, Real>) * WPB <= 9 * HM * HM * 8 + 16 * 1024, "cold_in_lds() LDS estimate");
+    static_assert(sizeof(Shared<HM, NWM, Real>) * WPB + cold_bytes<HM, MAXT, CS, QL, GL, FL, Real>() <= 160 * 1024,
+                  "LDS of one workgroup");
     __shared__ Shared<HM, NWM, Real> shv[WPB];
     auto& sh = shv[grp<GL>()];
     const int b = blockIdx.x * WPB + grp<GL>();
@@ -1748,30 +1755,41 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
     //      finiteness (a non-finite yhat or an overflowing R -> solver_error) ----
     Real mx = Real(0.0);
     bool finite = true;
-#pragma unroll
-    for (int t = 0; t < HM; ++t) {
-        T.m[t] = Real(0.0);
-        if (T.act && t < H) {
-            T.m[t] = np_expm1_d(yh[t * N + T.i]);
-            finite = finite && isfinite(T.m[t]);
-            mx = fmax(mx, fabs(T.m[t]));
-        }
-    }
-    if (T.act) finite = finite && isfinite(T.wpi);
-    mx = R.max1(mx);
-    const Real nonfinite = R.max1(finite ? Real(0.0) : Real(1.0));
-    // a period whose every R underflowed to 0 (yhat <= -103.97): R_t . w_t = 0 on the whole simplex,
-    // and the reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy reports infeasible
-    // (sum of R >= 0 over the assets: zero iff every R is zero)
     bool r_zero = false;
     {
-        Real rs[HM];
+        Real rs[HM];   // per period S_t = sum_i R_t,i of the float32 R
 #pragma unroll
-        for (int t = 0; t < HM; ++t) rs[t] = (T.act && t < H) ? Real(1.0) + T.m[t] : Real(0.0);
+        for (int t = 0; t < HM; ++t) {
+            T.m[t] = rs[t] = Real(0.0);
+            if (T.act && t < H) {
+                const float r = np_expf(yh[t * N + T.i]);
+                T.m[t] = (Real)((double)r - 1.0);
+                rs[t] = (Real)r;
+                finite = finite && isfinite(T.m[t]);
+            }
+        }
+        if (T.act) finite = finite && isfinite(T.wpi);
         R.periods(rs);
+        // S_t = 0 (every R underflowed, yhat <= -103.97): R_t . w_t = 0 on the whole simplex and the
+        // reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy reports infeasible.
+        // 0 < S_t < TINY_PERIOD (every yhat below ~ -11): the program is the same for R_t / S_t up to
+        // the constant log S_t, and m = R - 1 would round to -1 (R below 2^-53), so that period runs
+        // on m = R / S_t - 1 and the objective adds log S_t back (sh.lsc; oracle: kmpc_oracle_solve)
 #pragma unroll
-        for (int t = 0; t < HM; ++t) r_zero = r_zero || (t < H && rs[t] == Real(0.0));
+        for (int t = 0; t < HM; ++t) {
+            r_zero = r_zero || (t < H && rs[t] == Real(0.0));
+            if (T.act && t < H && rs[t] > Real(0.0) && rs[t] < Real(TINY_PERIOD))
+                T.m[t] = (Real)((double)np_expf(yh[t * N + T.i]) / (double)rs[t] - 1.0);
+            if (T.act && t < H) mx = fmax(mx, fabs(T.m[t]));
+        }
+        if (gvt<GL>() == 0) {
+#pragma unroll
+            for (int t = 0; t < HM; ++t)
+                sh.lsc[t] = (t < H && rs[t] > Real(0.0) && rs[t] < Real(TINY_PERIOD)) ? (Real)log((double)rs[t]) : Real(0.0);
+        }
     }
+    mx = R.max1(mx);
+    const Real nonfinite = R.max1(finite ? Real(0.0) : Real(1.0));
     Real sig = fmax(mx, Real(args.c));
     if (!(sig > Real(0.0))) sig = Real(1.0);
     T.sig = sig;
@@ -2080,7 +2098,7 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
             if (PH != 1 && best < huge_of<Real>()) {
                 // problem.value (mpc.py:103) at the best iterate: sum_t log(R_t . w_t) - c ||w_t - w_{t-1}||_1
                 Real f = Real(0.0);
-                for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) - args.c * sh.best_l1[t];
+                for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) + sh.lsc[t] - args.c * sh.best_l1[t];
                 best_obj = f;
             }
             if (best <= Real(1e-7)) status = KMPC_STATUS_OPTIMAL;

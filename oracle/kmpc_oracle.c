@@ -110,6 +110,9 @@ void kmpc_oracle_gross_returns(long n, const float* y, float* R) {
     for (long k = 0; k < n; ++k) R[k] = np_expf(y[k]);
 }
 
+/* a period whose gross returns sum below this is solved on R / sum(R) (see kmpc_oracle_solve) */
+#define KMPC_TINY_PERIOD 0x1p-16
+
 #define ST_OPTIMAL 0
 #define ST_INACCURATE 1
 #define ST_INFEASIBLE 2
@@ -536,21 +539,29 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
         W.n_refine = 3;   /* the kernels' default (kmpc_solve_desc.n_refine = 0 -> 3) */
         real sig = c;
         for (int i = 0; i < N; ++i) W.wp[i] = wp[i];
-        for (size_t k = 0; k < HN; ++k) {
-            W.m[k] = (real)((double)np_expf(yhat[k]) - 1.0);   /* exact: R has 24 bits */
-            if (RFABS(W.m[k]) > sig) sig = RFABS(W.m[k]);
+        for (size_t k = 0; k < HN; ++k)
+            W.m[k] = (real)((double)np_expf(yhat[k]) - 1.0);   /* exact for R >= 2^-29: R has 24 bits */
+
+        /* per period S_t = sum_i R_t,i of the float32 R.
+           S_t = 0 (every R underflowed: yhat <= -103.97): R_t . w_t = 0 on the whole simplex and the
+           reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy reports infeasible
+           (mpc.py:113: fallback, value None).
+           0 < S_t < 2^-16 (every yhat below ~ -11): the program is the same for R_t / S_t up to the
+           constant log S_t (log(R.w) = log S_t + log((R / S_t).w)), and 1 + m = R would lose R's
+           digits (m = R - 1 rounds to -1 below 2^-53), so m = R / S_t - 1 there (KMPC_TINY_PERIOD,
+           as the kernels; the objective below is evaluated from R itself) */
+        for (int t = 0; t < H; ++t) {
+            double S = 0;
+            for (int i = 0; i < N; ++i) S += (double)np_expf(yhat[t * N + i]);
+            if (S == 0) { status = ST_INFEASIBLE; goto done; }
+            if (S < KMPC_TINY_PERIOD)
+                for (int i = 0; i < N; ++i)
+                    W.m[t * N + i] = (real)((double)np_expf(yhat[t * N + i]) / S - 1.0);
         }
+        for (size_t k = 0; k < HN; ++k)
+            if (RFABS(W.m[k]) > sig) sig = RFABS(W.m[k]);
         if (!(sig > 0)) sig = 1;
         W.sig = sig; W.c = c / sig; W.tau = tau;
-
-        /* a period whose every R is 0 (yhat <= -103.97 underflows np.exp): R_t . w_t = 0 on the
-           whole simplex and the reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy
-           reports infeasible (mpc.py:113: fallback, value None) */
-        for (int t = 0; t < H; ++t) {
-            int zero = 1;
-            for (int i = 0; i < N; ++i) zero &= W.m[t * N + i] == -1;
-            if (zero) { status = ST_INFEASIBLE; goto done; }
-        }
 
         if (allow_short && !W.hs) {
             /* no bounds and no turnover terms: unbounded unless every period is flat */

@@ -150,3 +150,25 @@ def test_float32_gross_return_ties_decide_the_optimum():
     # with float64 exp the larger yhat would win up to the cap
     Wd, _ = dense_ipm.dense_ipm([0.5, 0.5], y, 0.0, 0.2)
     assert np.abs(Wd[0] - 0.5).max() < 1e-6
+
+
+def test_tiny_gross_return_period_is_optimal():
+    """A period whose every yhat is ~ -50 (R ~ 2e-22 > 0): optimal, solved on R / sum(R)
+    (KMPC_TINY_PERIOD), with the same plan as the unshifted window and an objective 50 lower per
+    shifted period (float32 rounding of yhat - 50 aside); every R exactly 0 stays infeasible."""
+    from oracle import solver as o
+    rng = np.random.default_rng(1)
+    N, H = 20, 4
+    wp = rng.dirichlet(np.ones(N))
+    y = rng.normal(5e-4, 0.015, (H, N)).astype(np.float32)
+    y2 = y.copy()
+    y2[2] -= 50
+    for c, tau in ((1e-3, 0.2), (0.0, 0.3), (0.0, 0.0)):
+        W, s, f, _ = o.solve(wp, y, c, tau)
+        W2, s2, f2, _ = o.solve(wp, y2, c, tau)
+        assert s == 0 and s2 == 0
+        assert abs(f2 + 50 - f) < 5e-6
+        assert np.abs(W[0] - W2[0]).max() < 1e-6
+    y3 = y.copy()
+    y3[1] = -110.0
+    assert o.solve(wp, y3, 1e-3, 0.2)[1] == 2

@@ -20,9 +20,10 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _solve(wp, y, c, tau, short=False, full=True, path=0):
+def _solve(wp, y, c, tau, short=False, full=True, path=0, precision="auto"):
     H = y.shape[1]
-    cfg = MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, allow_short=short, solver_path=path)
+    cfg = MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, allow_short=short, solver_path=path,
+                    precision=precision)
     W, st, val = solve_mpc_log_utility_batched(torch.tensor(wp, device="cuda"), torch.tensor(y, device="cuda"),
                                                cfg, return_full=full)
     return W.cpu().numpy(), st.cpu().numpy(), val.cpu().numpy()
@@ -342,3 +343,35 @@ def test_large_window_slot_reuse(N, H, B):
     assert (sto <= 1).all()
     assert np.abs(val[idx] - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
     assert np.abs(W[idx] - Wo[:, 0]).max() < 1e-3
+
+
+@pytest.mark.parametrize("N,H,c,tau,path", [(3, 2, 0.0, 0.0, 0),      # presolve, register fast path
+                                            (80, 20, 0.0, 0.0, 0),    # presolve, general loop
+                                            (3, 2, 1e-3, 0.2, 0),     # packed interior point
+                                            (100, 10, 1e-3, 0.2, 0),  # C3 case (float32 phase + float64)
+                                            (100, 10, 1e-3, 0.2, -1),  # C3 case, float64 only
+                                            (70, 7, 0.0, 0.0, 1),     # register kernel, no presolve
+                                            (300, 12, 1e-3, 0.2, 0)])  # large-window kernel
+def test_tiny_gross_return_period_is_solved(N, H, c, tau, path):
+    """a period whose every yhat is ~ -50 has R ~ 2e-22 > 0. The reference's program
+    is feasible and optimal there (log(R.w) is finite), but m = R - 1 rounds to -1 in float64, so
+    the interior points used to report it infeasible while the presolve said optimal. Every path now
+    solves such a period on R / sum(R) (TINY_PERIOD) and adds log sum(R) back: the same status on
+    every path (optimal), the oracle's objective, and the shift property — the window equals the
+    unshifted one with that period's objective lowered by 50 (float32 rounding of yhat - 50 aside)."""
+    rng = np.random.default_rng(N * 7 + H)
+    wp = rng.dirichlet(np.ones(N), 2)
+    y = rng.normal(5e-4, 0.015, (2, H, N)).astype(np.float32)
+    y2 = y.copy()
+    y2[1, H - 1, :] -= 50.0
+    prec = "f64" if path < 0 else "auto"
+    path = max(path, 0)
+    W, st, val = _solve(wp, y2, c, tau, path=path, precision=prec)
+    Wu, stu, valu = _solve(wp, y, c, tau, path=path, precision=prec)
+    Wo, sto, valo, _ = oracle.solve_batch(wp, y2, c, tau)
+    assert (st == 0).all() and (sto == 0).all(), (st, sto)
+    assert np.abs(val - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
+    assert abs((val[1] + 50.0) - valu[1]) < 5e-5            # float32 yhat - 50 keeps ~4e-6 of yhat
+    assert np.array_equal(W[0], Wu[0])                       # the other window is untouched
+    if c > 0:
+        assert np.abs(W[1, 0] - Wu[1, 0]).max() < 1e-3
