@@ -46,14 +46,28 @@ def run(y, cfg):
     return best, W, s, v, it
 
 
+from oracle import solver as oracle
+NCHK = int(os.environ.get("NCHK", "256"))
+ORACLE = {}
+for name, y in (("bench", y_bench), ("random", y_rand)):   # long-double oracle on the first NCHK windows
+    Wo, sto, vo, _ = oracle.solve_batch(wp[:NCHK].cpu().numpy(), y[:NCHK].cpu().numpy(), 1e-3, 0.2, precision="ld")
+    ORACLE[name] = (torch.tensor(Wo[:, 0], device=dev), torch.tensor(vo, device=dev))
+
+
+def vs_oracle(name, W, v):
+    Wo, vo = ORACLE[name]
+    return (f"oracle[{NCHK}]: max|dobj| {(v[:NCHK] - vo).abs().max().item():.2e} "
+            f"max|dW0| {(W[:NCHK] - Wo).abs().max().item():.2e}")
+
+
 for name, y in (("bench", y_bench), ("random", y_rand)):
     dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64"))
     print(f"[{name}] f64: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters {it64.float().mean().item():.2f} "
-          f"status {np.bincount(s64.cpu().numpy(), minlength=5)}", flush=True)
+          f"status {np.bincount(s64.cpu().numpy(), minlength=5)} {vs_oracle(name, W64, v64)}", flush=True)
     for mu in MUS:
         dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu))
         ok = (s <= 1) & (s64 <= 1)
         print(f"[{name}] mixed mu_handoff={mu:g}: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters "
               f"{it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)} "
               f"max|dobj| {(v - v64)[ok].abs().max().item():.3e} max|dW0| {(W - W64)[ok].abs().max().item():.3e} "
-              f"status==f64 {int((s == s64).sum().item())}/{B}", flush=True)
+              f"status==f64 {int((s == s64).sum().item())}/{B} {vs_oracle(name, W, v)}", flush=True)
