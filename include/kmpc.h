@@ -131,9 +131,14 @@ int kmpc_gross_returns(size_t n, const float* yhat, float* R, void* stream);
 #define KMPC_NORM_ID   0
 #define KMPC_NORM_BALL 1
 #define KMPC_MAX_LAYERS 8
-#define KMPC_DTYPE_F32  0
-#define KMPC_DTYPE_BF16 1
-
+#define KMPC_DTYPE_F32  0   /* fp32 arithmetic (the reference's). The GEMMs run on the bf16 MFMA with
+                               each fp32 operand split exactly into three bf16 planes and the six
+                               leading plane products accumulated in fp32: an fp32 GEMM in accuracy
+                               (error against a float64 restatement equal to the f32-input MFMA's,
+                               DESIGN.md §3.1), 2.7x the f32-input MFMA's peak rate               */
+#define KMPC_DTYPE_BF16 1   /* GEMM operands rounded to bf16 (BASELINE configs[4])               */
+#define KMPC_DTYPE_F32_F32MFMA 2   /* fp32 arithmetic on the f32-input MFMA (v_mfma_f32_32x32x2_f32,
+                                      the round-4 GEMMs; A/B and tests)                          */
 /*
  * An MLP (model.py:67-117, MLPCoder): n_layers Linear layers with dims[0] -> dims[1] -> ... ->
  * dims[n_layers]; activation `act` after every layer but the last; ReLU after the last one when
@@ -176,9 +181,9 @@ typedef struct kmpc_rollout_desc {
                                  rows i .. i+d-1 (kmpc_standardize below) — the time-delay
                                  embedding without materialising it; the first encoder layer's
                                  column blocks must then be in oldest-lag-first order.          */
-    int dtype;                /* KMPC_DTYPE_F32 (0, the reference's arithmetic) or KMPC_DTYPE_BF16 (1:
-                                 GEMM operands rounded to bf16 on MFMA, fp32 accumulation and
-                                 epilogues; BASELINE configs[4])                                 */
+    int dtype;                /* KMPC_DTYPE_F32 (0, the reference's fp32 arithmetic), KMPC_DTYPE_BF16
+                                 (1: GEMM operands rounded to bf16 on MFMA, fp32 accumulation and
+                                 epilogues; BASELINE configs[4]) or KMPC_DTYPE_F32_F32MFMA (2)   */
     int latent_unfused;       /* 0: the H-step loop runs as one fused launch where the model allows
                                  it; 1: one GEMM launch per step (same arithmetic; A/B and tests)  */
 } kmpc_rollout_desc;

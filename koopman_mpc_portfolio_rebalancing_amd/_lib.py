@@ -22,7 +22,7 @@ KMPC_MAX_H = 21          # the Schur system (3H rows) is factored by one 64-lane
 MODEL_GENERIC, MODEL_LISTA = 0, 1
 ACT = {"relu": 0, "tanh": 1, "gelu": 2}
 NORM = {"id": 0, "ball": 1}
-DTYPE = {"fp32": 0, "bf16": 1}
+DTYPE = {"fp32": 0, "bf16": 1, "fp32_f32mfma": 2}
 
 STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
                 4: "solver_error"}

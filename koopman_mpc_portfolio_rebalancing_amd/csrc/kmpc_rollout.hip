@@ -7,10 +7,11 @@
 //     yhat[:, k, :] = decode(z)[:, :N] * std + mean      model.py:768-777 / 839-850,
 //                                          data_finance.py:729 (slice), :740-742 (de-standardize)
 //
-// Every dense contraction is one fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32: exact fp32 products,
-// fp32 accumulation, the arithmetic type of the reference's torch fp32 path) — or, with
-// desc->dtype = KMPC_DTYPE_BF16, a bf16 MFMA GEMM (operands rounded to bf16, fp32 accumulation;
-// BASELINE configs[4]) — with a fused epilogue
+// Every dense contraction is one fp32 GEMM — the arithmetic type of the reference's torch fp32
+// path — on the bf16 MFMA with each fp32 operand split exactly into three bf16 planes
+// (gemm_nt_x3_kernel; desc->dtype = KMPC_DTYPE_F32, the default) or on the f32-input MFMA
+// (v_mfma_f32_32x32x2_f32, KMPC_DTYPE_F32_F32MFMA); or, with KMPC_DTYPE_BF16, a bf16 MFMA GEMM
+// (operands rounded to bf16, fp32 accumulation; BASELINE configs[4]) — with a fused epilogue
 // (bias + activation, LISTA shrink, de-standardize-and-scatter). Only the first N decoder rows are
 // evaluated. Weights in the reference's nn.Linear [out, in] layout are consumed as-is ("NT");
 // K and S (right-multiplied, [in, out]) are transposed once per call into the workspace.
@@ -44,7 +45,8 @@ struct GemmArgs {
     const float* R; int ldr;      // EPI_SHRINK addend [M, N]
     float thr;
     const float* mean; const float* stdv;   // EPI_DESTD [N]
-    int bf16;                     // 1: operands rounded to bf16, v_mfma_f32_32x32x16_bf16 (fp32 accumulate)
+    int bf16;                     // 1: operands rounded to bf16, v_mfma_f32_32x32x16_bf16 (fp32 accumulate);
+                                  // 2: fp32 operands as three bf16 planes (gemm_nt_x3_kernel)
     int ksplit;                   // > 1: blockIdx.z takes a K slice, raw partials to part[z][M][N]
     float* part;                  //      (splitk_epilogue_kernel sums them in slice order, then the epilogue)
 };
@@ -382,6 +384,197 @@ __global__ void __launch_bounds__(256) gemm_nt_bf16_kernel(GemmArgs g) {
     epilogue<WT, WT>(g, acc, m0, n0, wm, wn, lane);
 }
 
+// fp32 GEMM as three bf16 planes (round 5): every fp32 operand x is split exactly into
+// x = hi + mid + lo, three bf16 numbers (8 significant bits each, 24 in all: hi = bf16(x),
+// mid = bf16(x - hi), lo = x - hi - mid, every subtraction exact in fp32), and
+//   a . b = sum over the six plane pairs of order <= 2^-16:  hi.hi + hi.mid + mid.hi + hi.lo + lo.hi + mid.mid
+// on v_mfma_f32_32x32x16_bf16 (bf16 x bf16 products are exact in fp32, fp32 accumulation). The
+// dropped pairs (mid.lo, lo.mid, lo.lo) are below 2^-24 of |a b|: the same order as the one fp32
+// rounding of an fp32 product, so the result is an fp32 GEMM in accuracy (measured against an fp64
+// reference beside the native f32-input MFMA: tests/test_rollout_gpu.py) at 12 MFMA cycles per k
+// instead of 32 (v_mfma_f32_32x32x2_f32: 64 cycles for k = 2; the bf16 form: 32 cycles for k = 16).
+// Same tiles, k loop (register double buffering), split-K and epilogues as gemm_nt_kernel; the
+// planes are formed while staging into LDS.
+#ifndef KMPC_F32_GEMM   // the GEMM form of KMPC_DTYPE_F32: 2 three bf16 planes, 0 f32-input MFMA (dev A/B)
+#define KMPC_F32_GEMM 2
+#endif
+#ifndef KMPC_X3_TIMING   // dev timing bounds only (wrong results): 1 no split, 2 half the products
+#define KMPC_X3_TIMING 0
+#endif
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)x;
+    if (KMPC_X3_TIMING == 1) { mid = hi; lo = hi; return; }
+    const float r1 = x - (float)hi;
+    mid = (__bf16)r1;
+    lo = (__bf16)(r1 - (float)mid);
+}
+
+#ifndef KMPC_X3_DB   // 1: two LDS buffers, the next k-tile split between this tile's MFMA steps
+#define KMPC_X3_DB 1
+#endif
+template <int WM, int WN, int GM = 2, int GN = 2>
+__global__ void __launch_bounds__(64 * GM * GN) gemm_nt_x3_kernel(GemmArgs g) {
+    constexpr int NT = 64 * GM * GN;
+    constexpr int TM = 32 * GM * WM, TN = 32 * GN * WN;
+    constexpr int BKT = BK;                    // 32: two 16-k MFMA steps per k-tile
+    constexpr int LS = BKT + 8;                // bf16 elements per LDS row (80 B: aligned ds_read_b128)
+    // two buffers when they fit and the workgroup alone holds four waves per SIMD (a smaller one
+    // keeps the single buffer: two workgroups per CU share the LDS; dev A/B tools/ab_x3.sh)
+    constexpr bool DB = KMPC_X3_DB && 2 * 3 * (TM + TN) * LS * 2 <= 160 * 1024 && GM * GN >= 16;
+    constexpr int NB = DB ? 2 : 1;
+    __shared__ __bf16 As[NB][3][TM * LS];
+    __shared__ __bf16 Bs[NB][3][TN * LS];
+    static_assert(sizeof(As) + sizeof(Bs) <= 160 * 1024, "LDS");
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int m0, n0;
+    xcd_tile(m0, n0, TM, TN);
+    const int wm = (wv / GN) * 32 * WM, wn = (wv % GN) * 32 * WN;
+    f32x16 acc[WM][WN];
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+    const bool vec_ok = ((g.lda & 3) == 0) && ((g.ldb & 3) == 0) &&
+                        ((((uintptr_t)g.A) & 15) == 0) && ((((uintptr_t)g.B) & 15) == 0);
+    int kbeg = 0, kend = g.K;
+    if (g.ksplit > 1) {
+        const int kc = ((g.K + g.ksplit * BKT - 1) / (g.ksplit * BKT)) * BKT;
+        kbeg = blockIdx.z * kc;
+        kend = min(g.K, kbeg + kc);
+    }
+    constexpr int QA = TM * BKT / (4 * NT), QB = TN * BKT / (4 * NT);
+    static_assert(QA * 4 * NT == TM * BKT && QB * 4 * NT == TN * BKT, "tile loads per thread");
+    constexpr int RQ = BKT / 4;
+    f32x4 va[QA], vb[QB];
+    auto fetch_row = [&](const float* P, int ld, int rows, int r0, int row, int kk, f32x4& v) {
+        v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int rr = r0 + row;
+        if (rr >= rows) return;
+        if (vec_ok && kk + 3 < kend) {
+            v = *(const f32x4*)(P + (size_t)rr * ld + kk);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (kk + e < kend) v[e] = P[(size_t)rr * ld + kk + e];
+        }
+    };
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int idx = tid + q * NT;
+            fetch_row(g.A, g.lda, g.M, m0, idx / RQ, k0 + (idx % RQ) * 4, va[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int idx = tid + q * NT;
+            fetch_row(g.B, g.ldb, g.N, n0, idx / RQ, k0 + (idx % RQ) * 4, vb[q]);
+        }
+    };
+    auto put = [&](__bf16* S0, __bf16* S1, __bf16* S2, int idx, const f32x4& v) {
+        bf16x4 h, m, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            __bf16 x0, x1, x2;
+            split3(v[e], x0, x1, x2);
+            h[e] = x0; m[e] = x1; l[e] = x2;
+        }
+        const int o = (idx / RQ) * LS + (idx % RQ) * 4;
+        *(bf16x4*)(S0 + o) = h;
+        *(bf16x4*)(S1 + o) = m;
+        *(bf16x4*)(S2 + o) = l;
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < QA; ++q) put(As[buf][0], As[buf][1], As[buf][2], tid + q * NT, va[q]);
+#pragma unroll
+        for (int q = 0; q < QB; ++q) put(Bs[buf][0], Bs[buf][1], Bs[buf][2], tid + q * NT, vb[q]);
+    };
+    auto substep = [&](int buf, int st) {   // lane (r, h): k = 16 st + 8 h + j
+        const int r = lane & 31, h = lane >> 5;
+        {
+            bf16x8 af[3][WM], bf[3][WN];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int a = 0; a < WM; ++a)
+                    af[p][a] = *(const bf16x8*)(As[buf][p] + (wm + a * 32 + r) * LS + 16 * st + 8 * h);
+#pragma unroll
+                for (int b = 0; b < WN; ++b)
+                    bf[p][b] = *(const bf16x8*)(Bs[buf][p] + (wn + b * 32 + r) * LS + 16 * st + 8 * h);
+            }
+#pragma unroll
+            for (int a = 0; a < WM; ++a)
+#pragma unroll
+                for (int b = 0; b < WN; ++b) {
+                    // the small pairs first, hi.hi last (fixed order: deterministic)
+                    f32x16 c = acc[a][b];
+                    if (KMPC_X3_TIMING == 2) {
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[2][b], c, 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], c, 0, 0, 0);
+                        continue;
+                    }
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], c, 0, 0, 0);   // mid.mid
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], c, 0, 0, 0);   // lo.hi
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], c, 0, 0, 0);   // hi.lo
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], c, 0, 0, 0);   // mid.hi
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], c, 0, 0, 0);   // hi.mid
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], c, 0, 0, 0);   // hi.hi
+                    acc[a][b] = c;
+                }
+        }
+    };
+    if constexpr (DB) {
+        // one barrier per k-tile: tile k's MFMA steps read buffer k & 1 while tile k + 1 (fetched
+        // into registers one iteration earlier) is split into the other buffer between them
+        fetch(kbeg);
+        stage(0);
+        if (kbeg + BKT < kend) fetch(kbeg + BKT);
+        __syncthreads();
+        int buf = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+            substep(buf, 0);
+            if (k0 + BKT < kend) {
+                stage(buf ^ 1);
+                if (k0 + 2 * BKT < kend) fetch(k0 + 2 * BKT);
+            }
+            substep(buf, 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    } else {
+        fetch(kbeg);
+        for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+            stage(0);
+            __syncthreads();
+            if (k0 + BKT < kend) fetch(k0 + BKT);
+            substep(0, 0);
+            substep(0, 1);
+            __syncthreads();
+        }
+    }
+    if (g.ksplit > 1) {   // raw partial of this K slice
+        float* P = g.part + (size_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+            for (int b = 0; b < WN; ++b) {
+                const int n = n0 + wn + b * 32 + (lane & 31);
+                if (n >= g.N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < g.M) P[(size_t)m * g.N + n] = acc[a][b][r];
+                }
+            }
+        return;
+    }
+    epilogue<WM, WN>(g, acc, m0, n0, wm, wn, lane);
+}
+
 // shrink in place (LISTA initial z = shrink(c, thr), model.py:203)
 __global__ void shrink_kernel(const float* x, float* y, size_t n, float thr) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -664,7 +857,7 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) 
 // LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
 // descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
 static bool latent_fusable(const kmpc_rollout_desc* d) {
-    return !d->latent_unfused && d->dtype == KMPC_DTYPE_F32 && d->decoder.n_layers == 1 && d->L % 32 == 0 &&
+    return !d->latent_unfused && d->dtype != KMPC_DTYPE_BF16 && d->decoder.n_layers == 1 && d->L % 32 == 0 &&
            d->L <= 512 && ((uintptr_t)d->decoder.weight[0] & 15) == 0 &&
            !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn != KMPC_NORM_ID && d->norm_fn != KMPC_NORM_BALL);
 }
@@ -703,12 +896,21 @@ constexpr size_t SPLITK_ELEMS = (size_t)256 * 64 * 64;
 #endif
 // nparts (optional): a split-K layer with no epilogue (EPI_NONE) leaves its raw partials in part and
 // reports the slice count instead of launching splitk_epilogue_kernel (the latent kernels sum them)
+// an fp32 GEMM launch: the f32-input MFMA kernel, or (g.bf16 == 2) the same tile on three bf16 planes
+template <int WM, int WN, int GM = 2, int GN = 2>
+static void launch_f32(dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if (g.bf16 == 2)
+        hipLaunchKernelGGL((gemm_nt_x3_kernel<WM, WN, GM, GN>), grid, dim3(64 * GM * GN), 0, s, g);
+    else
+        hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, BK, GM, GN>), grid, dim3(64 * GM * GN), 0, s, g);
+}
+
 static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr, int* nparts = nullptr) {
     if (nparts) *nparts = 0;
     if (g.M <= 0 || g.N <= 0) return KMPC_OK;
     g.ksplit = 1;
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM);
-    if (g.bf16) {
+    if (g.bf16 == 1) {
         // fewer 128 x 128 tiles than CUs (BASELINE configs[4]: 1,024 windows x 512 -> 32 tiles) with a
         // long K: SPLITK slices, summed in slice order by the epilogue kernel (deterministic)
         const bool few = (size_t)grid.x * grid.y < 256;
@@ -733,7 +935,7 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr, int* nparts = 
         if (part && (size_t)grid64.x * grid64.y < 256 && g.K >= 128 * SPLITK) {
             g.ksplit = SPLITK;
             g.part = part;
-            hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), dim3(grid64.x, grid64.y, SPLITK), dim3(256), 0, s, g);
+            launch_f32<1, 1>(dim3(grid64.x, grid64.y, SPLITK), s, g);
             if (nparts && g.epi == EPI_NONE) {
                 *nparts = SPLITK;
                 return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
@@ -743,25 +945,25 @@ static int gemm(GemmArgs g, hipStream_t s, float* part = nullptr, int* nparts = 
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
         if (KMPC_GEMM_MID == 21)
-            hipLaunchKernelGGL((gemm_nt_kernel<2, 1>), dim3((g.N + 63) / 64, (g.M + 127) / 128), dim3(256), 0, s, g);
+            launch_f32<2, 1>(dim3((g.N + 63) / 64, (g.M + 127) / 128), s, g);
         else if (KMPC_GEMM_MID == 12)
-            hipLaunchKernelGGL((gemm_nt_kernel<1, 2>), dim3((g.N + 127) / 128, (g.M + 63) / 64), dim3(256), 0, s, g);
+            launch_f32<1, 2>(dim3((g.N + 127) / 128, (g.M + 63) / 64), s, g);
         else if (KMPC_GEMM_MID == 22)
-            hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
+            launch_f32<2, 2>(grid, s, g);
         else if (KMPC_GEMM_MID == 42)   // 128 x 128, 8 waves of 32 x 64
-            hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
+            launch_f32<1, 2, 4, 2>(grid, s, g);
         else if (KMPC_GEMM_MID == 44)   // 128 x 128, 16 waves of 32 x 32
-            hipLaunchKernelGGL((gemm_nt_kernel<1, 1, BK, 4, 4>), grid, dim3(1024), 0, s, g);
+            launch_f32<1, 1, 4, 4>(grid, s, g);
         else
-            hipLaunchKernelGGL((gemm_nt_kernel<1, 1>), grid64, dim3(256), 0, s, g);
+            launch_f32<1, 1>(grid64, s, g);
     } else if (KMPC_GEMM_BIG == 42) {   // 128 x 128, 8 waves of 32 x 64
-        hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 4, 2>), grid, dim3(512), 0, s, g);
+        launch_f32<1, 2, 4, 2>(grid, s, g);
     } else if (KMPC_GEMM_BIG == 44) {   // 128 x 128, 16 waves of 32 x 32
-        hipLaunchKernelGGL((gemm_nt_kernel<1, 1, BK, 4, 4>), grid, dim3(1024), 0, s, g);
+        launch_f32<1, 1, 4, 4>(grid, s, g);
     } else if (KMPC_GEMM_BIG == 82) {   // 256 x 128, 16 waves of 32 x 64
-        hipLaunchKernelGGL((gemm_nt_kernel<1, 2, BK, 8, 2>), dim3((g.N + 127) / 128, (g.M + 255) / 256), dim3(1024), 0, s, g);
+        launch_f32<1, 2, 8, 2>(dim3((g.N + 127) / 128, (g.M + 255) / 256), s, g);
     } else {
-        hipLaunchKernelGGL((gemm_nt_kernel<2, 2>), grid, dim3(256), 0, s, g);
+        launch_f32<2, 2>(grid, s, g);
     }
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
@@ -835,8 +1037,10 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (d->model_kind == KMPC_MODEL_LISTA && !d->lista_S) return KMPC_ERR_INVALID;
     if (ws_bytes < rollout_workspace_bytes(d) || (!ws && ws_bytes)) return KMPC_ERR_WORKSPACE;
     if (d->obs_ld < 0 || (d->obs_ld > 0 && d->obs_ld < d->N)) return KMPC_ERR_INVALID;
-    if (d->dtype != KMPC_DTYPE_F32 && d->dtype != KMPC_DTYPE_BF16) return KMPC_ERR_INVALID;
-    const int bf = d->dtype == KMPC_DTYPE_BF16;
+    if (d->dtype != KMPC_DTYPE_F32 && d->dtype != KMPC_DTYPE_BF16 && d->dtype != KMPC_DTYPE_F32_F32MFMA)
+        return KMPC_ERR_INVALID;
+    // GemmArgs::bf16: 2 = three bf16 planes (fp32 arithmetic), 1 = bf16 operands, 0 = f32-input MFMA
+    const int bf = d->dtype == KMPC_DTYPE_F32 ? KMPC_F32_GEMM : d->dtype == KMPC_DTYPE_BF16 ? 1 : 0;
     if (d->B == 0) return KMPC_OK;
     const int Bn = d->B, L = d->L, N = d->N, H = d->H;
     const int obs_ld = d->obs_ld > 0 ? d->obs_ld : d->obs;

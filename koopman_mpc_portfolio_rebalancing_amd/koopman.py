@@ -112,8 +112,10 @@ class DeviceKoopman:
 
     def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None, dtype: str = "fp32",
                  fuse_latent: bool = True):
-        """dtype: 'fp32' (the reference's arithmetic, default) or 'bf16' (GEMM operands rounded to
-        bf16 on the bf16 MFMA, fp32 accumulation — BASELINE configs[4]). fuse_latent=False runs the
+        """dtype: 'fp32' (the reference's arithmetic, default: GEMMs on the bf16 MFMA with every fp32
+        operand split exactly into three bf16 planes — an fp32 GEMM in accuracy), 'fp32_f32mfma' (the
+        same arithmetic on the f32-input MFMA) or 'bf16' (GEMM operands rounded to bf16 on the bf16
+        MFMA, fp32 accumulation — BASELINE configs[4]). fuse_latent=False runs the
         H-step loop as one GEMM launch per step (kmpc_rollout_desc.latent_unfused; A/B and tests)."""
         self.fuse_latent = bool(fuse_latent)
         if dtype not in _lib.DTYPE:

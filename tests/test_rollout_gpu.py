@@ -320,3 +320,46 @@ def test_fused_z0_is_never_read():
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], km.rollout(x, m, s, H, N))
+
+
+def _ref64(sd, x, H, N, mean, std):
+    """GenericKM (relu encoder, norm id, one-layer decoder) in float64 (torch CPU, double)."""
+    h = x.double()
+    for i, k in enumerate((0, 2, 4)):
+        h = h @ sd[f"encoder.network.{k}.weight"].double().T + sd[f"encoder.network.{k}.bias"].double()
+        if i < 2:
+            h = torch.relu(h)
+    K = sd["kmat"].double()
+    D = sd["decoder.network.0.weight"].double()[:N]
+    out = []
+    for _ in range(H):
+        h = h @ K
+        out.append((h @ D.T) * torch.as_tensor(std).double() + torch.as_tensor(mean).double())
+    return torch.stack(out, 1).numpy()
+
+
+@pytest.mark.parametrize("B,N,L,H,obs", [(4096, 30, 128, 5, 600),     # configs[1]: mid tiles + split-K
+                                         (8200, 100, 256, 3, 400)])   # C3 widths: large tiles, ragged
+def test_fp32_gemm_forms_against_float64(B, N, L, H, obs):
+    """dtype 'fp32' runs the GEMMs on the bf16 MFMA with each fp32 operand split exactly into three
+    bf16 planes (six plane products, fp32 accumulation); 'fp32_f32mfma' on the f32-input MFMA.
+    Both against a float64 restatement of the same model: the three-plane form must be an fp32 GEMM
+    in accuracy — max error within 1.5x the f32-input MFMA's (measured 0.8-1.0x: 8.2e-7 vs 9.0e-7
+    at configs[1], 8.7e-7 vs 9.2e-7 at C3) and under the 2e-6 bar of the reference goldens."""
+    import bench
+    sd = bench.make_state_dict(obs, L, 1024, seed=3)
+    x = torch.randn(B, obs, generator=torch.Generator().manual_seed(6))
+    mean = np.full(N, 5e-4, np.float32)
+    std = np.full(N, 0.015, np.float32)
+    ref = _ref64(sd, x, H, N, mean, std)
+    scale = np.abs(ref - mean).max()
+    err = {}
+    for dt in ("fp32_f32mfma", "fp32"):
+        km = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG), torch.device("cuda"), dtype=dt)
+        y = km.rollout(x.cuda(), mean, std, H, N).double().cpu().numpy()
+        err[dt] = float(np.abs(y - ref).max() / scale)
+        print(f"[rel] {dt} vs float64 {err[dt]:.3e}")
+        if dt == "fp32":
+            assert np.array_equal(y, km.rollout(x.cuda(), mean, std, H, N).double().cpu().numpy())   # deterministic
+    assert err["fp32"] <= 1.5 * err["fp32_f32mfma"] + 1e-8, err
+    assert err["fp32"] <= 2e-6, err
