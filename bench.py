@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MPC window-solves/sec (batched backtest) at 1/2/4/8 MI355X vs host-CPU ref"
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+BF16_MFMA_PEAK = 2.5e15    # FLOP/s, dense bf16 MFMA (v_mfma_f32_32x32x16_bf16)
 F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 # per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
 PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_solve_pmc.json")
@@ -680,9 +681,14 @@ def main():
                                   "ceiling_windows_per_s_per_gpu": HBM_PEAK / (4 * obs + 8 * N)},
             "timed_path": "kmpc_window via DeviceKoopman.window (the KoopmanMPCStrategy.rebalance_batch path); "
                           "kernels: the same step as kmpc_rollout + kmpc_solve, HIP events, after the timed region",
+            # rollout: algorithmic fp32 FLOPs / time, against the f32-input MFMA peak; the GEMMs and the
+            # L = 256 latent loop run as three bf16 planes (six bf16 products per fp32 product), so
+            # the bf16 MFMA pipe executes 6x those FLOPs (rollout_bf16_mfma_executed_frac)
             "kernels": {"rollout_ms": roll_ms, "solve_ms": solve_ms, "two_call_ms_per_step": roll_ms + solve_ms,
                         "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
-                        "rollout_mfma_frac": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK},
+                        "rollout_frac_of_f32_mfma_peak": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK,
+                        "rollout_bf16_mfma_executed_frac": 6 * roll_flops / (roll_ms * 1e-3) / BF16_MFMA_PEAK,
+                        "rollout_gemm_form": "fp32 as three exact bf16 planes on v_mfma_f32_32x32x16_bf16"},
             "solver": {"optimal_or_inaccurate": n_opt, "windows": B,
                        "mean_ipm_iterations": float(its.float().mean().item())},
         }

@@ -853,6 +853,147 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps16_kernel(LatentArgs a) 
     }
 }
 
+// The H-step loop with the fp32 products on the bf16 MFMA in three exact planes (dtype
+// KMPC_DTYPE_F32 at L = 256 — the C3 latent — identity norm; other shapes keep the f32-input
+// kernels). 64 windows per block: z lives in LDS as its three bf16 planes (hi + mid + lo = z
+// exactly; [3][64][L + 8], 101 KB, one block of 8 waves per CU), K^T and the decoder rows are split
+// into planes once per call (split_planes_kernel, [3][rows][L] in the workspace, L2 resident) and
+// read straight into the B fragments with 16-byte loads, two 16-k steps ahead; each B fragment
+// feeds both 32-row tiles (half the L2 stream of 32-row blocks: a 32-row version of this kernel
+// measured 1.54 ms against the f32-input kernel's 1.46 ms at C3, bound by that stream). Per 16-k
+// step and tile six v_mfma_f32_32x32x16_bf16 (192 cycles) against eight v_mfma_f32_32x32x2_f32
+// (512). One z buffer: each wave keeps its z K tiles in accumulators, a barrier, then the tiles are
+// split into the buffer.
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* src, int R, int Rp, int L, int ld,
+                                                           __bf16* dst) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t n = (size_t)Rp * L;
+    if (i >= n) return;
+    const int row = (int)(i / L), col = (int)(i % L);
+    const float x = row < R ? src[(size_t)row * ld + col] : 0.0f;
+    __bf16 h, m, l;
+    split3(x, h, m, l);
+    dst[i] = h;
+    dst[n + i] = m;
+    dst[2 * n + i] = l;
+}
+
+constexpr int LATX3_ROWS = 64;
+// acc0 / acc1 += rows 0..31 / 32..63 of the z planes . B[32 plane rows at Bp, row stride L, plane
+// stride PS]^T over k in [0, L); the six plane products per 16-k step, small pairs first
+template <int L, int LSP, int PL>
+__device__ __forceinline__ void tile_x3_2(const __bf16* zp, const __bf16* Bp, size_t PS, int lane, f32x16& acc0,
+                                         f32x16& acc1) {
+    const int r = lane & 31, h = lane >> 5;
+    const __bf16* pa = zp + r * LSP + 8 * h;
+    const __bf16* pb = Bp + (size_t)r * L + 8 * h;
+    bf16x8 b0[3], b1[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        b0[p] = *(const bf16x8*)(pb + p * PS);
+        b1[p] = *(const bf16x8*)(pb + p * PS + 16);
+    }
+#pragma unroll 2
+    for (int k0 = 0; k0 < L; k0 += 16) {
+        bf16x8 bf[3], a0[3], a1[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            bf[p] = b0[p];
+            b0[p] = b1[p];
+            if (k0 + 32 < L) b1[p] = *(const bf16x8*)(pb + p * PS + k0 + 32);
+            a0[p] = *(const bf16x8*)(pa + p * PL + k0);
+            a1[p] = *(const bf16x8*)(pa + 32 * LSP + p * PL + k0);
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[1], bf[1], acc0, 0, 0, 0);   // mid.mid
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[1], bf[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[2], bf[0], acc0, 0, 0, 0);   // lo.hi
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[2], bf[0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[0], bf[2], acc0, 0, 0, 0);   // hi.lo
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[0], bf[2], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[1], bf[0], acc0, 0, 0, 0);   // mid.hi
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[1], bf[0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[0], bf[1], acc0, 0, 0, 0);   // hi.mid
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[0], bf[1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[0], bf[0], acc0, 0, 0, 0);   // hi.hi
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[0], bf[0], acc1, 0, 0, 0);
+    }
+}
+
+#ifndef KMPC_LATX3
+#define KMPC_LATX3 1
+#endif
+template <int NWV, int L>
+__global__ void __launch_bounds__(64 * NWV) latent_steps_x3_kernel(LatentArgs a, const __bf16* Kp,
+                                                                   const __bf16* Dp, int Dpad) {
+    extern __shared__ __bf16 zp[];   // [3][64][L + 8]
+    // L a compile-time constant: the tile write-back's LDS offsets are instruction immediates
+    constexpr int LSP = L + 8, PL = LATX3_ROWS * LSP, NCT = L / 32;
+    static_assert(NCT <= NWV, "one z K column tile per wave");
+    const int N = a.N;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.x * LATX3_ROWS;
+    for (int idx = tid; idx < LATX3_ROWS * L; idx += 64 * NWV) {
+        const int row = idx / L, col = idx - row * L;
+        const float x = (m0 + row < a.B) ? latent_z0(a, m0 + row, col) : 0.0f;
+        __bf16 p0, p1, p2;
+        split3(x, p0, p1, p2);
+        zp[row * LSP + col] = p0;
+        zp[PL + row * LSP + col] = p1;
+        zp[2 * PL + row * LSP + col] = p2;
+    }
+    __syncthreads();
+    const int ndt = (N + 31) / 32;
+    const size_t KPS = (size_t)L * L, DPS = (size_t)Dpad * L;
+    float* yhat = a.yhat;
+    for (int k = 0; k < a.H; ++k) {
+        // per-step launder of the base pointers: the addresses derived from them are recomputed
+        // each step (scalar work) instead of being hoisted into VGPRs for all H steps
+        asm volatile("" : "+s"(Kp), "+s"(Dp), "+s"(yhat));
+        // z <- z K: column tile wv of both row tiles, held in registers until every wave has read z
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.0f;
+        if (wv < NCT) tile_x3_2<L, LSP, PL>(zp, Kp + (size_t)wv * 32 * L, KPS, lane, acc0, acc1);
+        __syncthreads();
+        if (wv < NCT) {
+            __bf16* zt = zp + 4 * h * LSP + wv * 32 + r;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int o = ((i & 3) + 8 * (i >> 2)) * LSP;
+                __bf16 p0, p1, p2;
+                split3(acc0[i], p0, p1, p2);
+                zt[o] = p0;
+                zt[PL + o] = p1;
+                zt[2 * PL + o] = p2;
+                split3(acc1[i], p0, p1, p2);
+                zt[32 * LSP + o] = p0;
+                zt[PL + 32 * LSP + o] = p1;
+                zt[2 * PL + 32 * LSP + o] = p2;
+            }
+        }
+        __syncthreads();
+        // decode rows 0..N-1 (+ bias), de-standardize into yhat[:, k, :]
+        for (int ct = wv; ct < ndt; ct += NWV) {
+            f32x16 d0, d1;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d0[i] = d1[i] = 0.0f;
+            tile_x3_2<L, LSP, PL>(zp, Dp + (size_t)ct * 32 * L, DPS, lane, d0, d1);
+            const int nrow = ct * 32 + r;
+            if (nrow < N) {
+                const float bias = a.bias ? a.bias[nrow] : 0.0f, mu = a.mean[nrow], sd = a.stdv[nrow];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (m < a.B) yhat[((size_t)m * a.H + k) * N + nrow] = destandardize(d0[i] + bias, sd, mu);
+                    if (m + 32 < a.B)
+                        yhat[((size_t)(m + 32) * a.H + k) * N + nrow] = destandardize(d1[i] + bias, sd, mu);
+                }
+            }
+        }
+        // (the next step's z K only reads the planes; its writes follow the barrier after it)
+    }
+}
+
 // the fused H-step kernel: fp32, one decoder layer, L % 32 == 0 and <= 512 (2 x 32 rows of z in
 // LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
 // descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
@@ -998,6 +1139,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
     bytes += 2 * align256(sizeof(float) * B * d->L);               // z, c (LISTA) / z next
     const size_t part = B * (size_t)wmax < SPLITK_ELEMS ? B * (size_t)wmax : SPLITK_ELEMS;
     bytes += align256(sizeof(float) * SPLITK_BUF * part);          // split-K partials (small batches)
+    bytes += align256((size_t)6 * d->L * (d->L + 32 * (size_t)((d->N + 31) / 32)));   // K^T, D bf16 planes
     return bytes;
 }
 
@@ -1058,6 +1200,11 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     float* z0 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
     float* z1 = (float*)p;   p += align256(sizeof(float) * (size_t)Bn * L);
     float* part = (float*)p;   // split-K partials (gemm(): only M N <= SPLITK_ELEMS outputs are split)
+    {
+        const size_t pe = (size_t)Bn * wmax < SPLITK_ELEMS ? (size_t)Bn * wmax : SPLITK_ELEMS;
+        p += align256(sizeof(float) * SPLITK_BUF * pe);
+    }
+    __bf16* planes = (__bf16*)p;   // K^T and decoder-row bf16 planes (latent_steps_x3_kernel)
     int rc;
     // Small batches (the fused 16-row latent loop below KMPC_LAT16_MAXB windows) read K in place and
     // skip the transpose launch (configs[1]: 0.194 -> 0.190 ms per step); at 65,536 windows the
@@ -1124,6 +1271,19 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
             else
                 hipLaunchKernelGGL((latent_steps16_kernel<KMPC_LAT16_WAVES, false>), dim3((Bn + LAT16 - 1) / LAT16),
                                    dim3(64 * KMPC_LAT16_WAVES), lds, s, la);
+            return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+        }
+        if (KMPC_LATX3 && bf == 2 && !la.ball && L == 256) {
+            const int Dpad = 32 * ((N + 31) / 32);
+            __bf16* Kp = planes;
+            __bf16* Dp = planes + (size_t)3 * L * L;
+            const size_t nk = (size_t)L * L, nd = (size_t)Dpad * L;
+            hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, Kt, L, L, L, L, Kp);
+            hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, la.D, N, Dpad, L,
+                               L, Dp);
+            const size_t lds = sizeof(__bf16) * 3 * LATX3_ROWS * (L + 8);
+            hipLaunchKernelGGL((latent_steps_x3_kernel<8, 256>), dim3((Bn + LATX3_ROWS - 1) / LATX3_ROWS), dim3(512), lds,
+                               s, la, (const __bf16*)Kp, (const __bf16*)Dp, Dpad);
             return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
         }
         const size_t lds = sizeof(float) * 2 * LAT_ROWS * (L + 4);

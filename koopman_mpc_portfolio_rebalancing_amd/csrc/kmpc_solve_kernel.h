@@ -100,9 +100,11 @@ struct PhaseClock {};
 #define KMPC_F32_PARK 0
 #endif
 #ifndef KMPC_REFINE_RTOL
-#define KMPC_REFINE_RTOL 1e-7
+#define KMPC_REFINE_RTOL 1e-6
 #endif
-// refinement stops at ||r||_inf <= REFINE_RTOL ||b||_inf (the oracle uses the same rule)
+// refinement stops at ||r||_inf <= REFINE_RTOL ||b||_inf. 1e-6 (round 5; the oracle keeps 1e-7):
+// C3 solve 81.9 -> 80.6 ms, float64-only 93.1 -> 91.9 ms, same statuses, objective within 1e-8 of
+// the long-double oracle as before (tools/ab_mixed.sh, tools/mixed_probe.py)
 constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
 // corrector refinement only once the complementarity is this small (the oracle uses the same rule):
 // 1e-6, and 1e-5 with shorting allowed — there the w-block has no barrier and the reduced system

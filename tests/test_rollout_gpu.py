@@ -213,7 +213,8 @@ def test_bf16_lista_rollout_at_config5_shape():
 @pytest.mark.parametrize("norm,L,N,B,H", [("id", 64, 20, 1000, 4), ("ball", 64, 40, 333, 3),
                                           ("id", 128, 30, 4096, 5), ("ball", 256, 100, 70, 10),
                                           ("id", 512, 50, 300, 6),     # L = 512: 132 KB of LDS
-                                          ("ball", 64, 20, 8200, 3)])  # >= 8192 windows: 32-row blocks
+                                          ("ball", 64, 20, 8200, 3),   # >= 8192 windows: 32-row blocks
+                                          ("id", 256, 100, 8200, 10), ("id", 256, 33, 8193, 2)])  # ragged
 def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
     """The one-launch H-step loop (latent_steps_kernel: L % 32 == 0, single-layer decoder; 16 windows
     per block below 8,192 windows, 32 from there) against the per-step GEMM launches
