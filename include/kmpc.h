@@ -73,7 +73,7 @@ extern "C" {
  *          kernel keeps each window's interior-point state there: (22 HM + 128) (64 ceil(N / 64))
  *          doubles per window slot, HM = 10 for H <= 10 and 21 past it (the compiled horizon
  *          bound, not H), for min(B, 768) slots when N <= 256, min(B, 512) otherwise.
- *          The mixed-precision pair (KMPC_PRECISION_AUTO) keeps one float32 iterate record per
+ *          The mixed-precision pair (AUTO at >= KMPC_MIXED_MIN_B windows, MIXED) keeps one float32 iterate record per
  *          window of a chunk of min(B, 131072) windows: (5 H N + 3 H + 16) floats rounded up to 64 B.
  *          Too little -> KMPC_ERR_WORKSPACE.
  */
@@ -82,13 +82,17 @@ extern "C" {
 #define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
 #define KMPC_PATH_REGISTER_UNPACKED 3   /* register kernels, one window per wave even for N <= 32
                                            (no lane-group packing); for A/B and tests             */
-/* Arithmetic of the interior point. AUTO: where a mixed-precision kernel pair exists (H = 10,
- * N <= 103, no short, c > 0 or tau > 0 with a cap: BASELINE configs[2..3]) the first iterations run
- * in float32 (half the registers, two waves per SIMD) until mu <= mu_handoff, and the float64 kernel
- * finishes from that iterate to the same tolerance and status rules as F64; elsewhere float64.
+/* Arithmetic of the interior point. MIXED: where a mixed-precision kernel pair exists (H = 10,
+ * 64 < N < 104, no short, c > 0 or tau > 0 with a cap: BASELINE configs[2..3]) the first iterations
+ * run in float32 (the whole state in registers, no spills) until mu <= mu_handoff, and the float64
+ * kernel finishes from that iterate to the same tolerance and status rules as F64; elsewhere
+ * float64. AUTO: MIXED from KMPC_MIXED_MIN_B windows per call (a throughput win), F64 below it
+ * (a latency-bound batch: the lock-step backtest's few paths finish sooner in float64 alone).
  * F64: float64 throughout. The answer's accuracy is that of the float64 finish either way. */
-#define KMPC_PRECISION_AUTO 0
-#define KMPC_PRECISION_F64  1
+#define KMPC_PRECISION_AUTO  0
+#define KMPC_PRECISION_F64   1
+#define KMPC_PRECISION_MIXED 2
+#define KMPC_MIXED_MIN_B 2048
 typedef struct kmpc_solve_desc {
     int    B;              /* number of independent problems (windows)           */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */
@@ -102,7 +106,7 @@ typedef struct kmpc_solve_desc {
     int    n_refine;       /* max iterative-refinement steps per Newton solve; refinement stops once
                               ||r||_inf <= 1e-7 ||b||_inf (<0 -> none, 0 -> default 3)             */
     int    path;           /* KMPC_PATH_* (0 = by shape). Per call: no process-wide switches      */
-    int    precision;      /* KMPC_PRECISION_* (ABI 0.3.0)                                        */
+    int    precision;      /* KMPC_PRECISION_* (ABI 0.3.0; MIXED 0.4.0)                           */
     double mu_handoff;     /* mixed precision: the float32 phase hands its iterate to the float64
                               solve once the scaled complementarity mu <= mu_handoff
                               (<= 0 -> default 5e-5)                                               */
@@ -288,7 +292,9 @@ const char* kmpc_strerror(int code);
 
 /* Library version string, "kmpc <ABI> (gfx950)". ABI 0.2.0 appended kmpc_solve_desc.path and
    kmpc_rollout_desc.latent_unfused; 0.3.0 appended kmpc_solve_desc.precision and .mu_handoff:
-   callers built against an older ABI must rebuild. */
+   callers built against an older ABI must rebuild. 0.4.0 added enum values only
+   (KMPC_PRECISION_MIXED, KMPC_DTYPE_F32_F32MFMA; AUTO precision now float64 below KMPC_MIXED_MIN_B
+   windows; KMPC_DTYPE_F32's GEMMs on three bf16 planes), no layout change. */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

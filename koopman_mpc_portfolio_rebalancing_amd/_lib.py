@@ -36,12 +36,14 @@ EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace
                     "kmpc_mv_workspace_bytes", "kmpc_gross_returns")
 
 PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
-PRECISION_AUTO, PRECISION_F64 = 0, 1   # kmpc_solve_desc.precision
+PRECISION_AUTO, PRECISION_F64, PRECISION_MIXED = 0, 1, 2   # kmpc_solve_desc.precision
+MIXED_MIN_B = 2048   # KMPC_MIXED_MIN_B: AUTO runs the mixed pair from this many windows per call
 
 # ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
 # kmpc_rollout_desc.latent_unfused, 0.3.0 kmpc_solve_desc.precision and .mu_handoff, so an older
-# library would read them past its structs' end
-ABI_VERSION = "0.3.0"
+# library would read them past its structs' end; 0.4.0 added enum values only (KMPC_PRECISION_MIXED,
+# KMPC_DTYPE_F32_F32MFMA), no layout change
+ABI_VERSION = "0.4.0"
 
 
 class KmpcError(RuntimeError):

@@ -206,8 +206,12 @@ def calculate_metrics(df: pd.DataFrame) -> Dict:
 METRIC_NAMES = ("Sharpe Ratio", "Max Drawdown", "Avg Turnover", "Final Value", "Total Return")
 
 
+PREROLL_CHUNK = 65536   # windows per batched rollout of run_backtest_lockstep(prerollout=True)
+
+
 def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
-                          mean, std, n_rows: Optional[int] = None, graph: bool = False) -> Dict[str, Any]:
+                          mean, std, n_rows: Optional[int] = None, graph: bool = False,
+                          prerollout: bool = True) -> Dict[str, Any]:
     """P independent backtests of the reference loop (backtest.py:133-219) run in lock step on the
     device: at every step one batched window launch (kmpc_window over the P
     paths) and one bookkeeping launch (kmpc_backtest_step); calculate_metrics per path at the end
@@ -222,6 +226,11 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
         graph: capture the whole step sequence in one HIP graph and replay it (no per-launch host
             overhead or inter-kernel gaps: the latency-bound small-P case); same launches, same
             results as the eager loop.
+        prerollout: the forecasts depend on the observations only (not on the weights the steps
+            carry), so every step's rollout runs up front as one batched kmpc_rollout over the
+            S x P windows (PREROLL_CHUNK windows per launch) and each step launches only the solve
+            (kmpc_solve); False: one fused kmpc_window per step. The rollout tiles differ with the
+            batch size, so the two agree to fp32 summation order, not bit for bit.
     Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
         reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
     """
@@ -247,9 +256,20 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
     L = _lib.load()
     d = _lib.BacktestDesc(P, N, max(S, 1), float(config.cost_coeff))
 
+    H = int(strategy.mpc_config.horizon)
+    sc = max(1, PREROLL_CHUNK // P)          # steps per batched rollout
+    steps_t = torch.as_tensor(steps, dtype=torch.long, device=dev)
+
     def run_steps():
+        y = None
         for k, t in enumerate(steps):
-            W0, _, _ = km.window(xt[t], w, m, sd, N, strategy.mpc_config)
+            if prerollout:
+                if k % sc == 0:   # the forecasts of steps k .. k + sc - 1 in one launch
+                    n = min(sc, S - k)
+                    y = km.rollout(xt[steps_t[k:k + n]].reshape(n * P, -1), m, sd, H, N).reshape(n, P, H, N)
+                W0, _, _ = solve_mpc_log_utility_batched(w, y[k % sc], strategy.mpc_config)
+            else:
+                W0, _, _ = km.window(xt[t], w, m, sd, N, strategy.mpc_config)
             rn = rt[t + 1] if t + 1 < T else None
             _lib.check(L.kmpc_backtest_step(ctypes.byref(d), k, W0.data_ptr(),
                                             rn.data_ptr() if rn is not None else None, w.data_ptr(),

@@ -17,7 +17,7 @@ int check_solve(const kmpc_solve_desc* d) {
     // c < 0 makes -c ||dw||_1 concave in the maximization: not DCP, cvxpy raises (mpc.py:66-103)
     if (d->cost_coeff < 0.0) return KMPC_ERR_INVALID;
     if (d->path < KMPC_PATH_AUTO || d->path > KMPC_PATH_REGISTER_UNPACKED) return KMPC_ERR_INVALID;
-    if (d->precision < KMPC_PRECISION_AUTO || d->precision > KMPC_PRECISION_F64) return KMPC_ERR_INVALID;
+    if (d->precision < KMPC_PRECISION_AUTO || d->precision > KMPC_PRECISION_MIXED) return KMPC_ERR_INVALID;
     if (!(d->mu_handoff < 1.0)) return KMPC_ERR_INVALID;   // (NaN too)
     return KMPC_OK;
 }
@@ -26,7 +26,7 @@ int check_solve(const kmpc_solve_desc* d) {
 
 extern "C" {
 
-const char* kmpc_version(void) { return "kmpc 0.3.0 (gfx950)"; }
+const char* kmpc_version(void) { return "kmpc 0.4.0 (gfx950)"; }
 
 const char* kmpc_strerror(int code) {
     switch (code) {

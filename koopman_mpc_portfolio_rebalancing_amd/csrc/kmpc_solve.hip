@@ -253,8 +253,13 @@ SolveArgs make_args(const kmpc_solve_desc* d) {
 // pair — the C3 kernel's (H = 10, 128 threads with N < 104, no short, c > 0 or tau > 0, cap).
 // Windows go through in chunks of at most WARM_CHUNK, one warm record each.
 constexpr int WARM_CHUNK = 131072;
+// AUTO takes the pair from KMPC_MIXED_MIN_B windows: below it a launch is latency-bound (the
+// slowest window's iterations), and float64 alone measured faster — lock-step backtest, C3 model,
+// path-steps/s (tools/lockstep_probe.py): P = 64 53.7 k mixed vs 56.1 k float64, P = 256 191 k vs
+// 206 k, P = 1,024 404 k vs 430 k, P = 4,096 539 k vs 513 k
 bool mixed_case(const SolveArgs& a, const kmpc_solve_desc* d) {
-    if (d->precision != KMPC_PRECISION_AUTO) return false;
+    if (d->precision == KMPC_PRECISION_F64) return false;
+    if (d->precision == KMPC_PRECISION_AUTO && a.B < KMPC_MIXED_MIN_B) return false;
     if (a.path != KMPC_PATH_AUTO && a.path != KMPC_PATH_REGISTER && a.path != KMPC_PATH_REGISTER_UNPACKED) return false;
     const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
     return fl7 && a.H == 10 && a.N > 64 && a.N < 104;

@@ -35,7 +35,7 @@ class MPCConfig:
     tol: float = 1e-9
     n_refine: int = 0  # 0 -> kernel default
     solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM, 3 register IPM without lane-group packing
-    precision: str = "auto"  # kmpc_solve_desc.precision: "auto" (float32 warm-start phase + float64 finish where available) or "f64"
+    precision: str = "auto"  # kmpc_solve_desc.precision: "mixed" (float32 warm-start phase + float64 finish where available), "f64", or "auto" (mixed from 2,048 windows per call, else f64)
     mu_handoff: float = 0.0  # float32 -> float64 handoff at mu <= mu_handoff (0 -> kernel default 5e-5)
 
 
@@ -51,9 +51,9 @@ def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.S
     d.n_refine = int(getattr(config, "n_refine", 0))
     d.path = int(getattr(config, "solver_path", 0))
     prec = getattr(config, "precision", "auto")
-    if prec not in ("auto", "f64"):
-        raise ValueError(f"precision must be 'auto' or 'f64' (got {prec!r})")
-    d.precision = _lib.PRECISION_AUTO if prec == "auto" else _lib.PRECISION_F64
+    if prec not in ("auto", "f64", "mixed"):
+        raise ValueError(f"precision must be 'auto', 'f64' or 'mixed' (got {prec!r})")
+    d.precision = {"auto": _lib.PRECISION_AUTO, "f64": _lib.PRECISION_F64, "mixed": _lib.PRECISION_MIXED}[prec]
     d.mu_handoff = float(getattr(config, "mu_handoff", 0.0))
     if d.cost_coeff < 0:
         # -c ||dw||_1 with c < 0 is not concave: the reference's cvxpy problem fails DCP and raises

@@ -123,7 +123,8 @@ def test_lockstep_paths_match_sequential_and_reference_runs():
         np.testing.assert_allclose(out["turnover"][p].cpu().numpy(), df["turnover"].values, rtol=1e-6, atol=1e-6)
 
 
-def test_lockstep_graph_replay_equals_eager_loop():
+@pytest.mark.parametrize("prerollout", [True, False])
+def test_lockstep_graph_replay_equals_eager_loop(prerollout):
     """run_backtest_lockstep(graph=True): the whole step sequence (window + bookkeeping launches of
     every step, then the metrics) captured in one HIP graph and replayed gives the eager loop's
     histories, weights and metrics bit for bit (C3-shaped model, 64 paths)."""
@@ -138,9 +139,35 @@ def test_lockstep_graph_replay_equals_eager_loop():
     r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
     mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
     cfg = BacktestConfig(horizon=H)
-    eager = run_backtest_lockstep(strat, x, r, cfg, mean, std)
-    graph = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=True)
+    eager = run_backtest_lockstep(strat, x, r, cfg, mean, std, prerollout=prerollout)
+    graph = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=True, prerollout=prerollout)
     for k in ("portfolio_value", "return", "turnover", "cost", "weights"):
         assert torch.equal(eager[k], graph[k]), k
     for k, v in eager["metrics"].items():
         assert torch.equal(v, graph["metrics"][k]), k
+
+
+def test_lockstep_prerollout_matches_per_step_windows(monkeypatch):
+    """prerollout=True (every step's forecasts from batched kmpc_rollout launches up front, then one
+    kmpc_solve per step) against one fused kmpc_window per step: the same program; the rollout's
+    GEMM tiles depend on the batch size, so the forecasts agree to fp32 summation order and the
+    histories to 1e-6. PREROLL_CHUNK = 128 windows: 2 steps per rollout launch (chunk edges)."""
+    import bench
+    from koopman_mpc_portfolio_rebalancing_amd import backtest as bt
+    dev = torch.device("cuda")
+    N, L, H, P, T = 100, 256, 10, 64, 19
+    obs_n = N * 20
+    spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(P, T, obs_n, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    ref = run_backtest_lockstep(strat, x, r, cfg, mean, std, prerollout=False)
+    monkeypatch.setattr(bt, "PREROLL_CHUNK", 128)
+    pre = run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    assert pre["return"].shape == ref["return"].shape == (P, T - H)
+    np.testing.assert_allclose(pre["portfolio_value"].cpu().numpy(), ref["portfolio_value"].cpu().numpy(), rtol=1e-6)
+    np.testing.assert_allclose(pre["turnover"].cpu().numpy(), ref["turnover"].cpu().numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(pre["weights"].cpu().numpy(), ref["weights"].cpu().numpy(), atol=1e-5)

@@ -46,17 +46,21 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d.cost_coeff, d.path = 0.0, 7           # unknown solver path
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
-    d.path, d.precision = 0, 2              # unknown precision
+    d.path, d.precision = 0, 3              # unknown precision
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d.precision, d.mu_handoff = 0, 1.5       # a handoff past mu = 1 is no handoff
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d.mu_handoff = 0.0
     # the mixed-precision pair (C3 shape) needs one float32 iterate record per window
-    d.B, d.N, d.H, d.cost_coeff, d.max_turnover = 1000, 100, 10, 1e-3, 0.2
+    d.B, d.N, d.H, d.cost_coeff, d.max_turnover, d.precision = 1000, 100, 10, 1e-3, 0.2, 2   # MIXED
     rec = ((16 + 5 * 10 * 100 + 3 * 10 + 15) // 16) * 16 * 4
     assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) >= 1000 * rec
     d.precision = 1
     assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 0
+    d.precision = 0                          # AUTO: float64 below KMPC_MIXED_MIN_B windows, the pair from it
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 0
+    d.B = _lib.MIXED_MIN_B
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) >= _lib.MIXED_MIN_B * rec
     d.B, d.N, d.H, d.cost_coeff, d.max_turnover, d.precision = 0, 5, 5, 0.0, 0.0, 0
     assert lib.kmpc_gross_returns(0, None, None, None) == 0
     assert lib.kmpc_gross_returns(4, None, None, None) == -1
@@ -175,3 +179,17 @@ def test_compat_shims_expose_reference_module_names():
         for name in ("mpc", "backtest"):
             sys.modules.pop(name, None)
         sys.modules.update(saved)
+
+
+def test_python_constants_match_the_header():
+    """The ctypes layer's enum values (_lib.py) against include/kmpc.h's #defines."""
+    from koopman_mpc_portfolio_rebalancing_amd import _lib
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "kmpc.h")).read()
+    defs = {k: int(v) for k, v in re.findall(r"#define\s+(KMPC_\w+)\s+(-?\d+)\b", hdr)}
+    assert defs["KMPC_PRECISION_AUTO"] == _lib.PRECISION_AUTO
+    assert defs["KMPC_PRECISION_F64"] == _lib.PRECISION_F64
+    assert defs["KMPC_PRECISION_MIXED"] == _lib.PRECISION_MIXED
+    assert defs["KMPC_MIXED_MIN_B"] == _lib.MIXED_MIN_B
+    assert defs["KMPC_DTYPE_F32"] == _lib.DTYPE["fp32"]
+    assert defs["KMPC_DTYPE_BF16"] == _lib.DTYPE["bf16"]
+    assert defs["KMPC_DTYPE_F32_F32MFMA"] == _lib.DTYPE["fp32_f32mfma"]

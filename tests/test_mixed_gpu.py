@@ -45,7 +45,7 @@ def test_mixed_equals_f64_at_the_bar_with_cold_windows():
     wp[13] = 0.0
     wp[13, 0] = 3.0                          # sum(w_prev) = 3: the cap makes the budget unreachable
     c, tau = 1e-3, 0.2
-    Wm, stm, vm, itm = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau), full=True)
+    Wm, stm, vm, itm = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, precision="mixed"), full=True)
     Wd, std_, vd, itd = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, precision="f64"), full=True)
     assert np.array_equal(stm, std_)
     assert stm[5] == 4 and stm[9] == 2 and stm[13] == 2
@@ -58,7 +58,8 @@ def test_mixed_equals_f64_at_the_bar_with_cold_windows():
     assert np.abs(Wm[ok, 0] - Wd[ok, 0]).max() < 1e-3
     assert _feasible(Wm[ok], wp[ok], tau)
     # run-to-run bit-identical
-    Wm2, stm2, vm2, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau), full=True)
+    Wm2, stm2, vm2, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=c, max_turnover=tau, precision="mixed"),
+                               full=True)
     assert np.array_equal(Wm, Wm2) and np.array_equal(vm, vm2, equal_nan=True)
     # iterations: float32 + float64 ones, about the float64-only count (tools/f32phase_probe.py)
     assert abs(itm[ok].mean() - itd[ok].mean()) < 2.0
@@ -77,7 +78,8 @@ def test_mixed_handoff_threshold_keeps_parity(mu_handoff):
     B, N, H = 256, 90, 10
     wp = rng.dirichlet(np.ones(N), B)
     y = rng.normal(5e-4, 0.02, (B, H, N)).astype(np.float32)
-    W, st, val, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=2e-3, max_turnover=0.3, mu_handoff=mu_handoff))
+    W, st, val, _ = _solve(wp, y, MPCConfig(horizon=H, cost_coeff=2e-3, max_turnover=0.3, mu_handoff=mu_handoff,
+                                            precision="mixed"))
     Wo, sto, valo, _ = oracle.solve_batch(wp, y, 2e-3, 0.3)
     assert (sto == 0).all() and (st <= 1).all()
     assert np.abs(val - valo).max() <= 1e-6 + 1e-5 * np.abs(valo).max()
@@ -91,7 +93,7 @@ def test_warm_records_chunk_boundary():
     B, N, H = 131072 + 96, 100, 10
     wp = rng.dirichlet(np.ones(N), B)
     y = rng.normal(5e-4, 0.015, (B, H, N)).astype(np.float32)
-    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, precision="mixed")   # (the 128 alone too)
     W, st, val, it = _solve(wp, y, cfg)
     assert (st == 0).all()
     lo = 131072 - 32

@@ -41,14 +41,17 @@ def _feasible(W, wp, tau, short, tol=1e-8):
     return bool(ok)
 
 
+# precision "auto" solves these golden batches (< KMPC_MIXED_MIN_B windows) in float64; "mixed"
+# forces the float32 phase + float64 finish where the shape has it (the C3-shaped goldens)
+@pytest.mark.parametrize("precision", ["auto", "mixed"])
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mpc_*_*.npz"))))
-def test_solver_matches_golden(path):
+def test_solver_matches_golden(path, precision):
     if path.endswith("mpc_kat.npz"):
         pytest.skip("KATs tested separately")
     g = np.load(path)
     c, tau, short = g["config"]
     short = bool(short)
-    W, st, val = _solve(g["w_prev"], g["yhat"], c, tau, short)
+    W, st, val = _solve(g["w_prev"], g["yhat"], c, tau, short, precision=precision)
     # optimal everywhere, the shorting golden included (pinned: every window reaches "optimal" since
     # the shorting refinement threshold REFINE_MU_SHORT; a status regression fails here)
     assert (st == 0).all(), st
@@ -63,8 +66,9 @@ def test_solver_matches_golden(path):
         assert np.abs(W[:, 0] - g["W"][:, 0]).max() < 1e-3
 
 
-@pytest.mark.parametrize("name", ["mpc_cfg3_N100_H10.npz", "mpc_cfg5_N500_H20.npz", "mpc_cfg1_N10_H5.npz"])
-def test_device_solutions_are_certified_optimal(name):
+@pytest.mark.parametrize("name,precision", [("mpc_cfg3_N100_H10.npz", "auto"), ("mpc_cfg3_N100_H10.npz", "mixed"),
+                                            ("mpc_cfg5_N500_H20.npz", "auto"), ("mpc_cfg1_N10_H5.npz", "auto")])
+def test_device_solutions_are_certified_optimal(name, precision):
     """The device's own W, certified by weak duality (oracle/certificate.py: the LP-optimal dual z
     for y = 1 / (R.w), no interior-point code): gap <= the objective parity bar 1e-6 + 1e-5 |f*|.
     This is W-parity as distance to the optimal set: it holds wherever on the optimal face the
@@ -72,7 +76,7 @@ def test_device_solutions_are_certified_optimal(name):
     from oracle import certificate
     g = np.load(os.path.join(GOLD, name))
     c, tau, _ = g["config"]
-    W, st, val = _solve(g["w_prev"], g["yhat"], c, tau)
+    W, st, val = _solve(g["w_prev"], g["yhat"], c, tau, precision=precision)
     assert (st == 0).all()
     for b in range(W.shape[0]):
         r = certificate.certify(W[b], g["w_prev"][b], g["yhat"][b], c, tau)
