@@ -99,6 +99,9 @@ struct PhaseClock {};
 #ifndef KMPC_F32_PARK
 #define KMPC_F32_PARK 0
 #endif
+#ifndef KMPC_F64_PARK   // dev A/B: 0 keeps w, s in registers across the float64 Newton solves
+#define KMPC_F64_PARK 1
+#endif
 #ifndef KMPC_REFINE_RTOL
 #define KMPC_REFINE_RTOL 1e-6
 #endif
@@ -2015,7 +2018,7 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
                     // so it stays in memory and the loads are not forwarded from the stores.
                     // (the float32 phase has registers to spare at one wave per SIMD: no parking
                     // unless KMPC_F32_PARK)
-                    constexpr bool PARK = sizeof(Real) == 8 || KMPC_F32_PARK;
+                    constexpr bool PARK = sizeof(Real) == 8 ? KMPC_F64_PARK : KMPC_F32_PARK;
                     Real park[2 * HM];
 #pragma unroll
                     for (int t = 0; t < HM; ++t) { park[t] = T.w[t]; park[HM + t] = T.s[t]; }

@@ -22,6 +22,7 @@ if os.environ.get("KMPC_DEV_LIB"):   # a variant library built by csrc/Makefile 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 MUS = [float(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1e-4,5e-5,2e-5").split(",")]
 REPS = int(os.environ.get("REPS", "3"))
+TOL = float(os.environ.get("TOL", "1e-9"))   # MPCConfig.tol (the interior point's complementarity tolerance)
 dev = torch.device("cuda", 0)
 N, L, H = 100, 256, 10
 obs = N * 20
@@ -61,11 +62,11 @@ def vs_oracle(name, W, v):
 
 
 for name, y in (("bench", y_bench), ("random", y_rand)):
-    dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64"))
+    dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64", tol=TOL))
     print(f"[{name}] f64: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters {it64.float().mean().item():.2f} "
           f"status {np.bincount(s64.cpu().numpy(), minlength=5)} {vs_oracle(name, W64, v64)}", flush=True)
     for mu in MUS:
-        dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu))
+        dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu, tol=TOL))
         ok = (s <= 1) & (s64 <= 1)
         print(f"[{name}] mixed mu_handoff={mu:g}: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters "
               f"{it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)} "
