@@ -134,6 +134,25 @@ struct Ref {
     __device__ __forceinline__ const Ref& operator+=(double v) const { return *this = (double)*this + v; }
 };
 
+// A float32-stored slab element (the first half of its array's rows, like the M array's R): the
+// factor-only arrays under KMPC_BIG_F32FAC (dev A/B: half the bytes of the arrays the Newton
+// sweeps read most; the float64 refinement against the unreduced system restores the direction)
+struct Ref32 {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned vo, so;
+    __device__ __forceinline__ operator double() const {
+        return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
+    }
+    __device__ __forceinline__ const Ref32& operator=(double v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0)), (float)v), rs, vo, so, 0);
+        return *this;
+    }
+};
+#ifndef KMPC_BIG_F32FAC
+#define KMPC_BIG_F32FAC 0
+#endif
+
 template <int HM, int FL>
 struct Win {
     const SolveArgs& a;
@@ -163,6 +182,14 @@ struct Win {
     __device__ __forceinline__ bool hs() const { return cs.hs; }
     __device__ __forceinline__ bool ht() const { return cs.ht; }
     __device__ __forceinline__ Ref at(int arr, int t) const { return Ref{rs, vo, (unsigned)((arr * HM + t) * NP) * 8u}; }
+    // the factor-only arrays (Lr, 1/Dd, P, BP): float32 under KMPC_BIG_F32FAC
+#if KMPC_BIG_F32FAC
+    __device__ __forceinline__ Ref32 fat(int arr, int t) const {
+        return Ref32{rs, vo >> 1, (unsigned)(arr * HM * NP) * 8u + (unsigned)(t * NP) * 4u};
+    }
+#else
+    __device__ __forceinline__ Ref fat(int arr, int t) const { return at(arr, t); }
+#endif
     // m = R - 1 of (t, i): the slab keeps the float32 R (exact: (double)R - 1 is the kernels' m) in
     // the first half of the M array's rows — half the bytes of the most-read input array
     __device__ __forceinline__ double mload(int t) const {
@@ -255,7 +282,7 @@ struct Win {
     }
     __device__ __forceinline__ double alpha(int t, double m) const { return m * sh.iden[t] * irsig; }
     __device__ __forceinline__ double eps(int t, const St& e) const { return ht() ? sh.sr[t] * e.bma * e.P : 0.0; }
-    __device__ __forceinline__ double epsa(int t) const { return ht() ? sh.sr[t] * at(A_BP, t) : 0.0; }
+    __device__ __forceinline__ double epsa(int t) const { return ht() ? sh.sr[t] * fat(A_BP, t) : 0.0; }
 
     // ---- reductions ----
     // wave total of v into this wave's partial slot j (every lane of the wave must call)
@@ -409,14 +436,14 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             mu_l += r1 + r2 + r3;
             rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
             P = cur.P;
-            W.at(A_P, t) = cur.P;
-            W.at(A_BP, t) = cur.bma * cur.P;
+            W.fat(A_P, t) = cur.P;
+            W.fat(A_BP, t) = cur.bma * cur.P;
             // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
             const double Dd = pi + (nx ? En : 0.0);
             ok = ok && (Dd > 0.0) && (Dd < 1e300);
             const double iDd = rcp(Dd);
-            W.at(A_IDD, t) = iDd;
-            W.at(A_LR, t) = lr;
+            W.fat(A_IDD, t) = iDd;
+            W.fat(A_LR, t) = lr;
             if (t) {
                 int ex;
                 pm = frexp(pm * fmax(lr, LR_FLOOR), &ex);
@@ -491,10 +518,10 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
         struct Gv { double idd, lr, m, bp; };
         auto ldG = [&](int t) {
             Gv v;
-            v.idd = W.at(A_IDD, t);
-            v.lr = W.at(A_LR, t);
+            v.idd = W.fat(A_IDD, t);
+            v.lr = W.fat(A_LR, t);
             v.m = W.mload(t);
-            v.bp = W.ht() ? (double)W.at(A_BP, t) : 0.0;
+            v.bp = W.ht() ? (double)W.fat(A_BP, t) : 0.0;
             return v;
         };
         Gv gnx{};
@@ -718,10 +745,10 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         auto ldR = [&](int t) {
             Rv v;
             v.r0 = W.at(A_R0, t);
-            v.lr = W.at(A_LR, t);
-            v.P = W.at(A_P, t);
+            v.lr = W.fat(A_LR, t);
+            v.P = W.fat(A_P, t);
             v.r1n = t + 1 < H ? (double)W.at(A_R1, t + 1) : 0.0;
-            v.bpn = t + 1 < H ? (double)W.at(A_BP, t + 1) : 0.0;
+            v.bpn = t + 1 < H ? (double)W.fat(A_BP, t + 1) : 0.0;
             return v;
         };
         Rv rn{};
@@ -729,7 +756,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         if (W.act) {
             rn = ldR(0);
             bsc = (double)W.at(A_R1, 0) - sh.lb5[0] * sh.iz4[0];
-            gpc = W.at(A_BP, 0) * bsc;
+            gpc = W.fat(A_BP, 0) * bsc;
         }
         for (int t = 0; t < H; ++t) {
             double pxv = 0.0;
@@ -767,7 +794,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         if (W.act) {
             const auto p = W.pre(0, corr, false);
             if (H > 1) pq = W.pre(1, corr, false);
-            lrc = W.at(A_LR, 0);
+            lrc = W.fat(A_LR, 0);
             cur = W.st(p, W.wpi);
             if (corr) {
                 dwc = p.dw;
@@ -787,7 +814,7 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 if (nx) {
                     const auto p = pq;
                     if (t + 2 < H) pq = W.pre(t + 2, corr, false);
-                    lrn = W.at(A_LR, t + 1);
+                    lrn = W.fat(A_LR, t + 1);
                     nxt = W.st(p, cur.w);
                     if (corr) {
                         dwn = p.dw;
@@ -897,12 +924,12 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         if (W.act && !fused) {
             // rhs_w -= g_t - g_{t+1}, g = bma P (bs - rho px); forward sweep y_t = x_t + Lr_t y_{t-1} (Y)
             double y = 0.0;
-            double gc = hs ? W.at(A_BP, 0) * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
+            double gc = hs ? W.fat(A_BP, 0) * (W.at(A_BS, 0) - sh.rho[0] * sh.px[0]) : 0.0;
             for (int t = 0; t < H; ++t) {
                 double gn = 0.0;
-                if (hs && t + 1 < H) gn = W.at(A_BP, t + 1) * (W.at(A_BS, t + 1) - sh.rho[t + 1] * sh.px[t + 1]);
+                if (hs && t + 1 < H) gn = W.fat(A_BP, t + 1) * (W.at(A_BS, t + 1) - sh.rho[t + 1] * sh.px[t + 1]);
                 const double x = W.at(A_BW, t) - gc + gn;
-                y = x + W.at(A_LR, t) * y;
+                y = x + W.fat(A_LR, t) * y;
                 W.at(A_Y, t) = y;
                 gc = gn;
             }
@@ -915,10 +942,10 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         auto ldB = [&](int t) {
             Bv v;
             v.y = W.at(A_Y, t);
-            v.idd = W.at(A_IDD, t);
-            v.bp = ht ? (double)W.at(A_BP, t) : 0.0;
+            v.idd = W.fat(A_IDD, t);
+            v.bp = ht ? (double)W.fat(A_BP, t) : 0.0;
             v.m = W.mload(t);
-            v.lr = W.at(A_LR, t);
+            v.lr = W.fat(A_LR, t);
             return v;
         };
         Bv bn{};
@@ -968,8 +995,8 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             auto ldF = [&](int t) {
                 Fv v;
                 v.m = W.mload(t);
-                v.bpn = (ht && t + 1 < H) ? (double)W.at(A_BP, t + 1) : 0.0;
-                v.lr = W.at(A_LR, t);
+                v.bpn = (ht && t + 1 < H) ? (double)W.fat(A_BP, t + 1) : 0.0;
+                v.lr = W.fat(A_LR, t);
                 return v;
             };
             Fv fn = ldF(0);
@@ -992,11 +1019,11 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
         auto ldC = [&](int t) {
             Cv v;
             v.y = W.at(A_Y, t);
-            v.idd = W.at(A_IDD, t);
-            v.lr = W.at(A_LR, t);
+            v.idd = W.fat(A_IDD, t);
+            v.lr = W.fat(A_LR, t);
             v.x = W.at(A_X, t);
-            v.bp = hs ? (double)W.at(A_BP, t) : 0.0;
-            v.P = hs ? (double)W.at(A_P, t) : 0.0;
+            v.bp = hs ? (double)W.fat(A_BP, t) : 0.0;
+            v.P = hs ? (double)W.fat(A_P, t) : 0.0;
             v.bs1 = (hs && t + 1 < H) ? (double)W.at(A_BS, t + 1) : 0.0;
             v.dwo = first ? 0.0 : (double)W.at(A_DW, t);
             v.ds1 = (!first && hs && t + 1 < H) ? (double)W.at(A_DS, t + 1) : 0.0;

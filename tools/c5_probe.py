@@ -16,3 +16,12 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     W, s, v, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
     torch.cuda.synchronize(); dt = time.time() - t
     print(f"N={N} H={H} B={B} {dt*1e3:.1f} ms {B/dt:.0f} win/s iters {it.float().mean().item():.2f}", flush=True)
+NCHK = int(os.environ.get("NCHK", "0"))   # > 0: the first NCHK windows against the long-double oracle
+print("status", np.bincount(s.cpu().numpy(), minlength=5), flush=True)
+if NCHK:
+    from oracle import solver as oracle
+    Wo, sto, vo, _ = oracle.solve_batch(wp[:NCHK].cpu().numpy(), y[:NCHK].cpu().numpy(), cfg.cost_coeff,
+                                        cfg.max_turnover, precision="ld")
+    print(f"oracle[{NCHK}]: status {np.bincount(sto, minlength=5)} max|dobj| "
+          f"{np.abs(v[:NCHK].cpu().numpy() - vo).max():.2e} max|dW0| {np.abs(W[:NCHK].cpu().numpy() - Wo[:, 0]).max():.2e}",
+          flush=True)
