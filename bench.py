@@ -546,6 +546,38 @@ def secondary_c5(dev, steps: int, warmup: int, B: int = 1024) -> dict:
                                   "meaning": "f*(fp32 yhat) - f(W_bf16; fp32 yhat), problem.value units"}}
 
 
+def rollout_f64(sd: dict, x: torch.Tensor, H: int, N: int, mean, std) -> np.ndarray:
+    """The bench model (GenericKM, relu encoder, identity norm, one-layer decoder) in float64 on the
+    CPU: the yardstick of the rollout's fp32 arithmetic (rollout_parity)."""
+    h = x.double().cpu()
+    for i, k in enumerate((0, 2, 4)):
+        h = h @ sd[f"encoder.network.{k}.weight"].double().T + sd[f"encoder.network.{k}.bias"].double()
+        if i < 2:
+            h = torch.relu(h)
+    K = sd["kmat"].double()
+    D = sd["decoder.network.0.weight"].double()[:N]
+    out = []
+    for _ in range(H):
+        h = h @ K
+        out.append((h @ D.T) * torch.as_tensor(std).double() + torch.as_tensor(mean).double())
+    return torch.stack(out, 1).numpy()
+
+
+def rollout_parity(model, sd, x, mean_d, std_d, H, N, n=512) -> dict:
+    """Max error of the timed rollout (fp32 GEMMs as three bf16 planes) and of the f32-input MFMA
+    form, against float64, relative to max|yhat - mean|, on the first n windows (after the timed
+    region)."""
+    from koopman_mpc_portfolio_rebalancing_amd import DeviceKoopman
+    ref = rollout_f64(sd, x[:n], H, N, mean_d.cpu().numpy(), std_d.cpu().numpy())
+    scale = float(np.abs(ref - mean_d.cpu().numpy()).max())
+    y3 = model.rollout(x[:n], mean_d, std_d, H, N).double().cpu().numpy()
+    native = DeviceKoopman(model.spec, model.device, dtype="fp32_f32mfma")
+    y1 = native.rollout(x[:n], mean_d, std_d, H, N).double().cpu().numpy()
+    return {"windows": n, "vs": "float64 restatement (torch CPU, double)",
+            "three_plane_max_rel_err": float(np.abs(y3 - ref).max() / scale),
+            "f32_input_mfma_max_rel_err": float(np.abs(y1 - ref).max() / scale)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -692,6 +724,7 @@ def main():
             "solver": {"optimal_or_inaccurate": n_opt, "windows": B,
                        "mean_ipm_iterations": float(its.float().mean().item())},
         }
+        line["rollout_parity"] = rollout_parity(model, sd, x, mean_d, std_d, H, N)
         if world == 1:
             line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
             line["secondary_c1"] = secondary_c1(dev, args.steps, args.warmup)
