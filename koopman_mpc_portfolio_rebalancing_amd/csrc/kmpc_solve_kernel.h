@@ -1808,7 +1808,6 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
     const int tw = args.return_full ? H : 1;   // periods written out
     double best_obj = __builtin_nan("");
     bool handoff = false;   // PH = 1: the iterate went to the window's warm record
-    bool warm_start = false;   // PH = 2: this window started from the float32 iterate
     int it0 = 0;            // PH >= 2: iterations of the earlier phases (reported with these)
 
     if (nonfinite == Real(0.0) && isfinite(args.c) && isfinite(args.tau)) {
@@ -1841,8 +1840,8 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
             const float* rec = nullptr;
             if constexpr (PH == 2) {
                 rec = args.warm + (size_t)b * warm_stride(H, N);
-                warm = reinterpret_cast<const int*>(rec)[0] == 1;
-                warm_start = warm;
+                // (a wave-uniform flag: a scalar branch; unchanged in memory until the end)
+                warm = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(rec)[0]) == 1;
             }
             if (warm) {
                 const float* st = rec + WARM_HEAD;
@@ -2157,9 +2156,10 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
         if constexpr (PH >= 2) {   // + the earlier phases' iterations (spent on a cold window too)
             int* hd = reinterpret_cast<int*>(args.warm + (size_t)b * warm_stride(H, N));
             it0 = hd[1];
-            // a warm start that did not end optimal: the retry pass (PH = 3) solves the window
-            // again from the usual initial point, so no status is worse than the float64-only one
-            if (PH == 2 && warm_start && status != KMPC_STATUS_OPTIMAL) {
+            // a warm start (header flag 1, re-read here rather than kept live across the loop)
+            // that did not end optimal: the retry pass (PH = 3) solves the window again from the
+            // usual initial point, so no status is worse than the float64-only one
+            if (PH == 2 && hd[0] == 1 && status != KMPC_STATUS_OPTIMAL) {
                 hd[0] = 3;
                 hd[1] = it + it0;
             }
