@@ -364,3 +364,47 @@ def test_fp32_gemm_forms_against_float64(B, N, L, H, obs):
             assert np.array_equal(y, km.rollout(x.cuda(), mean, std, H, N).double().cpu().numpy())   # deterministic
     assert err["fp32"] <= 1.5 * err["fp32_f32mfma"] + 1e-8, err
     assert err["fp32"] <= 2e-6, err
+
+
+def test_three_plane_paths_lista_and_unaligned_rows():
+    """The three-plane fp32 paths off the bench shapes, at >= 8,192 windows with L = 256 (the large
+    GEMM tiles and latent_steps_x3_kernel): (1) LISTAKM (linear We, 10 loops: the shrink-epilogue
+    GEMMs and the LISTA z0 into the plane latent loop); (2) GenericKM with obs = 99 (rows not a
+    multiple of 4 floats: the scalar operand fetch) and N = 33. Each against the numpy fp32
+    restatement and the f32-input MFMA form (1e-5 of the decoded scale, the fp32 rollout bars)."""
+    import bench
+    rng = np.random.default_rng(9)
+    B, L, H = 8200, 256, 4
+    # (1) LISTA
+    N, d = 64, 3
+    obs_n = N * d
+    We = (rng.standard_normal((L, obs_n)) / np.sqrt(obs_n)).astype(np.float32)
+    lip = 1.1 * np.linalg.norm(We.astype(np.float64), 2) ** 2
+    S = (np.eye(L) - We.astype(np.float64) @ We.astype(np.float64).T / lip).astype(np.float32)
+    q, _ = np.linalg.qr(rng.standard_normal((L, L)))
+    D = rng.standard_normal((L, obs_n)).astype(np.float32)
+    Dn = (D / np.maximum(np.linalg.norm(D, axis=1, keepdims=True), 1e-4)).astype(np.float32)
+    spec = KoopmanModelSpec(kind="lista", encoder=[(torch.from_numpy(We / np.float32(lip)), None)],
+                            kmat=torch.from_numpy((0.95 * q).astype(np.float32)),
+                            decoder=[(torch.from_numpy(Dn.T.copy()), None)], lista_S=torch.from_numpy(S),
+                            lista_loops=10, lista_thresh=float(5e-3 / lip))
+    obs = rng.standard_normal((B, obs_n)).astype(np.float32)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    y = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    y1 = DeviceKoopman(spec, torch.device("cuda"), dtype="fp32_f32mfma").rollout(
+        torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    ref = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
+    assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, "three-plane lista L256")
+    assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, "three-plane vs f32-input lista L256")
+    # (2) GenericKM, obs 99
+    N, obs_n = 33, 99
+    sd = bench.make_state_dict(obs_n, L, 512, seed=7)
+    spec = KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG)
+    obs = rng.standard_normal((B, obs_n)).astype(np.float32)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    y = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    y1 = DeviceKoopman(spec, torch.device("cuda"), dtype="fp32_f32mfma").rollout(
+        torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+    ref = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
+    assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, "three-plane generic obs99")
+    assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, "three-plane vs f32-input generic obs99")
