@@ -412,11 +412,12 @@ __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16&
 #ifndef KMPC_X3_DB   // 1: two LDS buffers, the next k-tile split between this tile's MFMA steps
 #define KMPC_X3_DB 1
 #endif
-template <int WM, int WN, int GM = 2, int GN = 2>
+template <int WM, int WN, int GM = 2, int GN = 2, int BKT = BK>
 __global__ void __launch_bounds__(64 * GM * GN) gemm_nt_x3_kernel(GemmArgs g) {
     constexpr int NT = 64 * GM * GN;
     constexpr int TM = 32 * GM * WM, TN = 32 * GN * WN;
-    constexpr int BKT = BK;                    // 32: two 16-k MFMA steps per k-tile
+    constexpr int NS = BKT / 16;               // 16-k MFMA steps per k-tile (BKT = 32: two)
+    static_assert(NS * 16 == BKT && NS >= 1, "k-tile of whole 16-k steps");
     constexpr int LS = BKT + 8;                // bf16 elements per LDS row (80 B: aligned ds_read_b128)
     // two buffers when they fit and the workgroup alone holds four waves per SIMD (a smaller one
     // keeps the single buffer: two workgroups per CU share the LDS; dev A/B tools/ab_x3.sh)
@@ -541,7 +542,8 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_nt_x3_kernel(GemmArgs g) {
                 stage(buf ^ 1);
                 if (k0 + 2 * BKT < kend) fetch(k0 + 2 * BKT);
             }
-            substep(buf, 1);
+#pragma unroll
+            for (int st = 1; st < NS; ++st) substep(buf, st);
             __syncthreads();
             buf ^= 1;
         }
@@ -551,8 +553,8 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_nt_x3_kernel(GemmArgs g) {
             stage(0);
             __syncthreads();
             if (k0 + BKT < kend) fetch(k0 + BKT);
-            substep(0, 0);
-            substep(0, 1);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) substep(0, st);
             __syncthreads();
         }
     }
