@@ -209,9 +209,17 @@ METRIC_NAMES = ("Sharpe Ratio", "Max Drawdown", "Avg Turnover", "Final Value", "
 PREROLL_CHUNK = 65536   # windows per batched rollout of run_backtest_lockstep(prerollout=True)
 
 
+# path groups on their own streams for latency-bound path counts (tools/lockstep_probe.py, C3
+# model, ms per step, 1 / 2 / 3 / 4 / 8 groups): P = 64 1.144 / 1.107 / 1.080 / 1.062 / 2.02 (eight
+# streams share the process's four hardware queues: serialised); P = 256 1.240 / 1.209 / — / 1.178;
+# P = 1,024 2.38 / 1.93 / — / 2.73, unsteady from run to run, so one group there
+LOCKSTEP_GROUPS = 4
+LOCKSTEP_GROUPS_MAX_P = 256
+
+
 def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
                           mean, std, n_rows: Optional[int] = None, graph: bool = False,
-                          prerollout: bool = True) -> Dict[str, Any]:
+                          prerollout: bool = True, groups: Optional[int] = None) -> Dict[str, Any]:
     """P independent backtests of the reference loop (backtest.py:133-219) run in lock step on the
     device: at every step one batched window launch (kmpc_window over the P
     paths) and one bookkeeping launch (kmpc_backtest_step); calculate_metrics per path at the end
@@ -231,6 +239,12 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
             S x P windows (PREROLL_CHUNK windows per launch) and each step launches only the solve
             (kmpc_solve); False: one fused kmpc_window per step. The rollout tiles differ with the
             batch size, so the two agree to fp32 summation order, not bit for bit.
+        groups: the paths split into this many contiguous groups, each stepping on its own HIP
+            stream (default LOCKSTEP_GROUPS up to LOCKSTEP_GROUPS_MAX_P paths, with prerollout and
+            without graph; else 1). A step's solve lasts as long as its slowest window, so
+            independent groups wait only for their own slowest path: the small-P backtest runs at
+            the groups' mean step time instead of the maximum over all paths. Every window is
+            solved by the same kernel as in one group, so the results are bit-identical.
     Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
         reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
     """
@@ -259,6 +273,12 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
     H = int(strategy.mpc_config.horizon)
     sc = max(1, PREROLL_CHUNK // P)          # steps per batched rollout
     steps_t = torch.as_tensor(steps, dtype=torch.long, device=dev)
+    if groups is None:
+        groups = LOCKSTEP_GROUPS if (prerollout and not graph and P <= LOCKSTEP_GROUPS_MAX_P) else 1
+    groups = max(1, min(int(groups), P))
+    if groups > 1 and (graph or not prerollout):
+        raise ValueError("path groups need prerollout=True and graph=False")
+    bounds = [(P * g) // groups for g in range(groups + 1)]
 
     def run_steps():
         y = None
@@ -278,8 +298,43 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
             _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), metrics.data_ptr(),
                                                _lib.stream_handle(dev)))
 
+    def run_groups():
+        """The same per-step launches, path group g on stream g: group g's step k waits only for
+        group g's step k - 1. The forecasts are rolled out on the calling stream, which every group
+        stream waits for; the metrics launch waits for every group."""
+        main = torch.cuda.current_stream(dev)
+        streams = [torch.cuda.Stream(dev) for _ in range(groups)]
+        descs = [_lib.BacktestDesc(bounds[g + 1] - bounds[g], N, max(S, 1), float(config.cost_coeff))
+                 for g in range(groups)]
+        for st in streams:
+            st.wait_stream(main)
+        y = None
+        for k, t in enumerate(steps):
+            if k % sc == 0:
+                n = min(sc, S - k)
+                for st in streams:       # the previous chunk's readers before its memory is reused
+                    main.wait_stream(st)
+                y = km.rollout(xt[steps_t[k:k + n]].reshape(n * P, -1), m, sd, H, N).reshape(n, P, H, N)
+                for st in streams:
+                    st.wait_stream(main)
+            rn = rt[t + 1] if t + 1 < T else None
+            for g, st in enumerate(streams):
+                g0, g1 = bounds[g], bounds[g + 1]
+                with torch.cuda.stream(st):
+                    W0, _, _ = solve_mpc_log_utility_batched(w[g0:g1], y[k % sc][g0:g1], strategy.mpc_config)
+                    _lib.check(L.kmpc_backtest_step(
+                        ctypes.byref(descs[g]), k, W0.data_ptr(), rn[g0:g1].data_ptr() if rn is not None else None,
+                        w[g0:g1].data_ptr(), value[g0:g1].data_ptr(), hist[g0:g1].data_ptr(), _lib.stream_handle(dev)))
+        for st in streams:
+            main.wait_stream(st)
+        if S:
+            _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), metrics.data_ptr(),
+                                               _lib.stream_handle(dev)))
+
     with torch.cuda.device(dev):
-        if graph and S:
+        if groups > 1 and S:
+            run_groups()
+        elif graph and S:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 run_steps()

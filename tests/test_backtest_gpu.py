@@ -171,3 +171,27 @@ def test_lockstep_prerollout_matches_per_step_windows(monkeypatch):
     np.testing.assert_allclose(pre["portfolio_value"].cpu().numpy(), ref["portfolio_value"].cpu().numpy(), rtol=1e-6)
     np.testing.assert_allclose(pre["turnover"].cpu().numpy(), ref["turnover"].cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(pre["weights"].cpu().numpy(), ref["weights"].cpu().numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("P,groups", [(64, 4), (61, 3)])
+def test_lockstep_path_groups_on_streams_equal_one_group(P, groups):
+    """run_backtest_lockstep(groups=G): the paths in G contiguous groups, each stepping on its own
+    HIP stream, against one group: every window goes through the same solve kernel, so histories,
+    weights and metrics are bit-identical (uneven groups at P = 61)."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, T = 100, 256, 10, 22
+    obs_n = N * 20
+    spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(P, T, obs_n, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    one = run_backtest_lockstep(strat, x, r, cfg, mean, std, groups=1)
+    grp = run_backtest_lockstep(strat, x, r, cfg, mean, std, groups=groups)
+    for k in ("portfolio_value", "return", "turnover", "cost", "weights"):
+        assert torch.equal(one[k], grp[k]), k
+    for k, v in one["metrics"].items():
+        assert torch.equal(v, grp["metrics"][k]), k

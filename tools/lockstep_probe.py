@@ -29,13 +29,16 @@ for P, T in CASES:
     for graph, pre, mu in [(g_ == '1', p_ == '1', mu) for g_ in os.environ.get('GRAPH', '0,1').split(',')
                            for p_ in os.environ.get('PRE', '1,0').split(',') for mu in MUS]:
         strat = strats[mu]
-        out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std, graph=graph,
-                                    prerollout=pre)   # warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        out = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=graph, prerollout=pre)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        S = out["return"].shape[1]
-        print(f"P={P} T={T} graph={graph} prerollout={pre} mu={mu}: {S} steps in {dt*1e3:.1f} ms -> {P*S/dt:.0f} path-steps/s, "
-              f"{dt/S*1e3:.3f} ms/step, final value mean {out['portfolio_value'][:, -1].mean().item():.1f}", flush=True)
+        for grp in [int(v) for v in os.environ.get("PATH_GROUPS", "1").split(",")]:
+            if grp > 1 and (graph or not pre):
+                continue
+            out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std, graph=graph,
+                                        prerollout=pre, groups=grp)   # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = run_backtest_lockstep(strat, x, r, cfg, mean, std, graph=graph, prerollout=pre, groups=grp)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            S = out["return"].shape[1]
+            print(f"P={P} T={T} graph={graph} prerollout={pre} mu={mu} groups={grp}: {S} steps in {dt*1e3:.1f} ms -> {P*S/dt:.0f} path-steps/s, "
+                  f"{dt/S*1e3:.3f} ms/step, final value mean {out['portfolio_value'][:, -1].mean().item():.1f}", flush=True)
