@@ -454,6 +454,34 @@ def secondary_c1(dev, steps: int, warmup: int, B: int = 65536) -> dict:
             "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
 
 
+def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
+    """SURVEY §8(f) row 1 at a small path count: P lock-stepped backtest paths
+    of the headline model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2) over T test rows,
+    run_backtest_lockstep with its defaults (forecasts rolled out up front, path groups on streams);
+    path-steps/s = P x steps / wall time of the second of two identical runs."""
+    from koopman_mpc_portfolio_rebalancing_amd import BacktestConfig, KoopmanModelSpec, KoopmanMPCStrategy, MPCConfig
+    from koopman_mpc_portfolio_rebalancing_amd.backtest import run_backtest_lockstep
+    N, L, H = 100, 256, 10
+    obs = N * 20
+    spec = KoopmanModelSpec.from_state_dict(make_state_dict(obs, L, 1024, seed=0), MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device=str(dev))
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(P, T, obs, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    S = int(out["return"].shape[1])
+    return {"workload": f"{P} lock-stepped backtest paths x {S} steps, C3 model ({N} assets, latent {L}, H={H}), "
+                        "run_backtest_lockstep defaults", "path_steps_per_s": P * S / el, "ms_per_step": el / S * 1e3,
+            "r04_path_steps_per_s": 30.5e3}
+
+
 def make_lista_state_dict(obs: int, L: int, seed: int = 0) -> dict:
     """LISTAKM layout (model.py:190-209, 804-850) with LINEAR_ENCODER: the classic LISTA start
     We = D / Lc, S = I - D D^T / Lc for a random unit-row dictionary D [L, obs], Lc = 1.1 ||D||_2^2
@@ -729,6 +757,7 @@ def main():
             line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
             line["secondary_c1"] = secondary_c1(dev, args.steps, args.warmup)
             line["secondary_c5"] = secondary_c5(dev, min(args.steps, 3), min(args.warmup, 1))
+            line["secondary_lockstep"] = secondary_lockstep(dev)
         if world == 1 and args.cpu_seconds > 0:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base

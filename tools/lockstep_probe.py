@@ -17,7 +17,8 @@ spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs, L, 1024, seed
 # MU: the solve's precision / float32 handoff per run ("f64" = float64 only; a number = mu_handoff)
 MUS = os.environ.get("MU", "5e-5").split(",")
 strats = {mu: KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2,
-                                                 **({"precision": "f64"} if mu == "f64" else {"mu_handoff": float(mu)})),
+                                                 **({"precision": "f64"} if mu == "f64" else
+                                                    {"precision": "mixed"} if mu == "mixed" else {"mu_handoff": float(mu)})),
                                  device="cuda") for mu in MUS}
 CASES = [tuple(int(v) for v in c.split('x')) for c in os.environ.get('CASES', '64x260,1024x260,8192x60').split(',')]
 for P, T in CASES:
