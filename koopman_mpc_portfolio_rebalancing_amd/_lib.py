@@ -147,6 +147,30 @@ def stream_handle(device: torch.device | None = None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_STREAMS: dict = {}
+
+
+def group_streams(n: int, device: torch.device) -> list:
+    """n HIP streams of their own for concurrent launch sequences (the lock-step path groups),
+    created back to back once per process and device. HIP hands the process's GPU_MAX_HW_QUEUES
+    hardware queues to streams round-robin in creation order, so n consecutive creations land on n
+    different queues (measured: tools/queue_probe.py); streams from torch's pool may share one,
+    and two streams on one queue run their kernels one after the other."""
+    import ctypes
+    key = torch.device(device).index or 0
+    if key not in _STREAMS or len(_STREAMS[key]) < n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        made = []
+        with torch.cuda.device(key):
+            for _ in range(max(n, 4)):
+                h = ctypes.c_void_p()
+                if hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1)) != 0:   # hipStreamNonBlocking
+                    raise KmpcError("hipStreamCreateWithFlags failed")
+                made.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", key)))
+        _STREAMS[key] = made
+    return _STREAMS[key][:n]
+
+
 def require_gpu(t: torch.Tensor) -> None:
     if not t.is_cuda:
         raise KmpcError("libkmpc kernels need device (HIP) tensors; got a CPU tensor")

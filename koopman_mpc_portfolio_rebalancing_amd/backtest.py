@@ -210,11 +210,12 @@ PREROLL_CHUNK = 65536   # windows per batched rollout of run_backtest_lockstep(p
 
 
 # path groups on their own streams for latency-bound path counts (tools/lockstep_probe.py, C3
-# model, ms per step, 1 / 2 / 3 / 4 / 8 groups): P = 64 1.144 / 1.107 / 1.080 / 1.062 / 2.02 (eight
-# streams share the process's four hardware queues: serialised); P = 256 1.240 / 1.209 / — / 1.178;
-# P = 1,024 2.38 / 1.93 / — / 2.73, unsteady from run to run, so one group there
-LOCKSTEP_GROUPS = 4
-LOCKSTEP_GROUPS_MAX_P = 256
+# model, ms per step, 1 / 2 / 3 groups): P = 64 1.144 / 1.111 / 1.084; P = 256 1.245 / 1.208 /
+# 1.188; P = 1,024 2.393 / 1.923 / 1.904. Three: the process has four hardware queues
+# (GPU_MAX_HW_QUEUES) and a fourth group's stream shared one of them with another group in the same
+# measurement (2.10 ms at P = 64: two groups serialised)
+LOCKSTEP_GROUPS = 3
+LOCKSTEP_GROUPS_MAX_P = 1024
 
 
 def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
@@ -240,8 +241,8 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
             (kmpc_solve); False: one fused kmpc_window per step. The rollout tiles differ with the
             batch size, so the two agree to fp32 summation order, not bit for bit.
         groups: the paths split into this many contiguous groups, each stepping on its own HIP
-            stream (default LOCKSTEP_GROUPS up to LOCKSTEP_GROUPS_MAX_P paths, with prerollout and
-            without graph; else 1). A step's solve lasts as long as its slowest window, so
+            stream (_lib.group_streams; default LOCKSTEP_GROUPS up to LOCKSTEP_GROUPS_MAX_P paths,
+            with prerollout and without graph; else 1). A step's solve lasts as long as its slowest window, so
             independent groups wait only for their own slowest path: the small-P backtest runs at
             the groups' mean step time instead of the maximum over all paths. Every window is
             solved by the same kernel as in one group, so the results are bit-identical.
@@ -303,7 +304,7 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
         group g's step k - 1. The forecasts are rolled out on the calling stream, which every group
         stream waits for; the metrics launch waits for every group."""
         main = torch.cuda.current_stream(dev)
-        streams = [torch.cuda.Stream(dev) for _ in range(groups)]
+        streams = _lib.group_streams(groups, dev)   # (one hardware queue each; torch's pool may share)
         descs = [_lib.BacktestDesc(bounds[g + 1] - bounds[g], N, max(S, 1), float(config.cost_coeff))
                  for g in range(groups)]
         for st in streams:

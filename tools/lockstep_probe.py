@@ -30,8 +30,8 @@ for P, T in CASES:
     for graph, pre, mu in [(g_ == '1', p_ == '1', mu) for g_ in os.environ.get('GRAPH', '0,1').split(',')
                            for p_ in os.environ.get('PRE', '1,0').split(',') for mu in MUS]:
         strat = strats[mu]
-        for grp in [int(v) for v in os.environ.get("PATH_GROUPS", "1").split(",")]:
-            if grp > 1 and (graph or not pre):
+        for grp in [None if v == "d" else int(v) for v in os.environ.get("PATH_GROUPS", "d").split(",")]:
+            if grp is not None and grp > 1 and (graph or not pre):
                 continue
             out = run_backtest_lockstep(strat, x[:, :H + 2], r[:, :H + 2], cfg, mean, std, graph=graph,
                                         prerollout=pre, groups=grp)   # warm-up
