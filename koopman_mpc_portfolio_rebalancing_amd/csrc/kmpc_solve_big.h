@@ -37,8 +37,21 @@ namespace kmpc {
 namespace big {
 
 constexpr int KP = 64;             // padded Schur width (3 HM <= 63)
-constexpr int LDG = 65;            // LDS row stride of G / L (conflict-free row and column reads)
 constexpr int NWX = 16;            // max waves per window (1024 threads)
+// G / L in LDS: packed lower triangle (row r at r (r + 1) / 2; every access is on or below the
+// diagonal), 16.3 KB instead of the 33.3 KB of a full row-stride-65 square — with the reduction
+// slots sized to the block's waves, a 512-thread window's LDS drops from 56.4 to 39.8 KB, room for
+// four windows per CU (KMPC_BIG_TRI 0: the square, dev A/B). Same speed at two
+// per CU (C5: 64.8 vs 64.4 ms). More windows per CU do not pay: the registers are the limit, not
+// the LDS — three per CU (<= 80 VGPRs) took C5 from 64.8 to 117.6 ms, four (64 VGPRs, 524 B of
+// scratch per lane) to 151.7 ms, with spill reloads inside the load-latency-bound sweeps; one per
+// CU 79.1 ms (r05, tools/ab_c5.sh)
+#ifndef KMPC_BIG_TRI
+#define KMPC_BIG_TRI 1
+#endif
+constexpr int LDG = 65;            // (square layout) row stride: conflict-free row and column reads
+constexpr int G_DOUBLES = KMPC_BIG_TRI ? KP * (KP + 1) / 2 : KP * LDG;
+__device__ __forceinline__ int gi(int r, int k) { return KMPC_BIG_TRI ? ((r * (r + 1)) >> 1) + k : r * LDG + k; }
 // windows in flight = workspace slabs: two workgroups per CU for the >= 512-thread blocks (the
 // slab stream is HBM-bound there: 768 slots measured -9% at N = 300, H = 15, equal at N = 500),
 // three (the LDS limit) for windows of <= 256 assets, which are latency-bound (N = 100, H = 20:
@@ -49,10 +62,15 @@ constexpr int NWX = 16;            // max waves per window (1024 threads)
 #ifndef KMPC_BIG_MAX_SLOTS_SMALL
 #define KMPC_BIG_MAX_SLOTS_SMALL 768
 #endif
+// 512-thread windows (256 < N <= 512): two per CU (see KMPC_BIG_TRI; dev A/B with KMPC_BIG_WPE)
+#ifndef KMPC_BIG_MAX_SLOTS_MID
+#define KMPC_BIG_MAX_SLOTS_MID 512
+#endif
 constexpr int MAX_SLOTS = KMPC_BIG_MAX_SLOTS;
 constexpr int MAX_SLOTS_SMALL = KMPC_BIG_MAX_SLOTS_SMALL;
+constexpr int MAX_SLOTS_MID = KMPC_BIG_MAX_SLOTS_MID;
 __host__ __device__ inline int slots_for(int B, int N) {
-    const int cap = N <= 256 ? MAX_SLOTS_SMALL : MAX_SLOTS;
+    const int cap = N <= 256 ? MAX_SLOTS_SMALL : (N <= 512 ? MAX_SLOTS_MID : MAX_SLOTS);
     return B < cap ? B : cap;
 }
 constexpr double LR_FLOOR = 1e-14;
@@ -82,16 +100,17 @@ struct BigArgs {
 };
 
 // LDS of the fused solves: the raw Gram's v-columns, c_t = sqrt(rho_t) px_t, per-wave px partials
-template <int HM>
-constexpr int fx_doubles() { return KP * HM + HM + NWX * HM; }
+template <int HM, int NW = NWX>
+constexpr int fx_doubles() { return KP * HM + HM + NW * HM; }
 
+// (allocated as LDS of bs_bytes<HM>(waves): red is the last member and only the block's waves'
+// rows of it exist)
 template <int HM>
 struct BigShared {
-    double G[KP * LDG];          // Schur matrix (lower triangle), then L (unit lower, strictly below)
+    double G[G_DOUBLES];         // Schur matrix (lower triangle), then L (unit lower, strictly below)
     double gid[KP];              // 1 / D of G = L D L^T
     double q[KP];                // Schur solution (period-major index 3t + type)
     double tot[KP];              // block-reduction totals (slots < 3 HM <= 63)
-    double red[NWX][KP];         // per-wave partial slots of a period reduction
     double sc[2][NWX][2];        // per-wave partials of scalar reductions (alternating)
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
@@ -100,7 +119,11 @@ struct BigShared {
     double pxa[HM];    // the direction's px summed over its solves: ds = P (DS - rho pxa), sum_i ds = pxa isp1
     double lsc[HM];    // log S_t of a period run on R / S_t (tiny gross returns), else 0
     int flag;
+    double red[NWX][KP];         // per-wave partial slots of a period reduction (rows < waves)
 };
+// LDS doubles of a BigShared whose blocks have nw waves (the red rows past nw cut off)
+template <int HM>
+constexpr int bs_doubles(int nw) { return (int)((sizeof(BigShared<HM>) - sizeof(double) * (NWX - nw) * KP + 7) / 8); }
 
 // state of one (t, i) with its slack-derived quantities (recomputed, never stored)
 struct St {
@@ -569,7 +592,7 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
         W.slot(0, W.act ? epn * epn * dqn : 0.0);   // (v_0, v_0) = eps_0^2 dq_0
     }
     W.finish(H);   // (its barriers also publish the generators to the workgroup)
-    if ((int)threadIdx.x < H) sh.G[(3 * threadIdx.x) * LDG + 3 * threadIdx.x] = sh.tot[threadIdx.x];
+    if ((int)threadIdx.x < H) sh.G[gi(3 * threadIdx.x, 3 * threadIdx.x)] = sh.tot[threadIdx.x];
 #ifndef KMPC_BIG_GRAM_SUPER
 #define KMPC_BIG_GRAM_SUPER 1
 #endif
@@ -581,7 +604,7 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
             if (j < K3 && l < K3) {
                 const int tj = j / 3, tyj = j - 3 * tj, tl = l / 3, tyl = l - 3 * tl;
                 const bool use = tj < tl || (tj == tl && tyj <= tyl && !(tyj == 0 && tyl == 0));
-                if (use) sh.G[l * LDG + j] = acc[r];
+                if (use) sh.G[gi(l, j)] = acc[r];
             }
         }
     };
@@ -650,7 +673,7 @@ __device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht, 
         if (gv && ht && r < K3) {
             for (int tau = 0; tau < H; ++tau) {
                 const int p = 3 * tau;
-                gv[r * HM + tau] = p <= r ? sh.G[r * LDG + p] : sh.G[p * LDG + r];
+                gv[r * HM + tau] = p <= r ? sh.G[gi(r, p)] : sh.G[gi(p, r)];
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -659,25 +682,25 @@ __device__ __forceinline__ void schur_factor(BigShared<HM>& sh, int H, bool ht, 
             for (int k = 0; k <= r; ++k) {
                 const int tyk = k % 3;
                 const bool kused = tyk != 0 || ht;
-                double v = (rused && kused) ? sh.G[r * LDG + k] : 0.0;
+                double v = (rused && kused) ? sh.G[gi(r, k)] : 0.0;
                 if (k == r) v += (ty != 2 || !rused) ? 1.0 : 0.0;
-                sh.G[r * LDG + k] = v;
+                sh.G[gi(r, k)] = v;
             }
         }
         __builtin_amdgcn_wave_barrier();
         bool bad = false;
         for (int j = 0; j < K3; ++j) {
-            const double d = sh.G[j * LDG + j];
+            const double d = sh.G[gi(j, j)];
             bad = bad || !(d > 0.0) || !(d < 1e300);
             const double id = rcp(fmax(d, 1e-300));
             if (r == j) sh.gid[j] = id;
             const bool below = r > j && r < K3;
-            const double l = below ? sh.G[r * LDG + j] * id : 0.0;
+            const double l = below ? sh.G[gi(r, j)] * id : 0.0;
             __builtin_amdgcn_wave_barrier();
             if (below)
-                for (int k = j + 1; k <= r; ++k) sh.G[r * LDG + k] = fma(-l, sh.G[k * LDG + j], sh.G[r * LDG + k]);
+                for (int k = j + 1; k <= r; ++k) sh.G[gi(r, k)] = fma(-l, sh.G[gi(k, j)], sh.G[gi(r, k)]);
             __builtin_amdgcn_wave_barrier();
-            if (below) sh.G[r * LDG + j] = l;
+            if (below) sh.G[gi(r, j)] = l;
             __builtin_amdgcn_wave_barrier();
         }
         if (bad && r == 0) sh.flag = 1;
@@ -707,13 +730,13 @@ __device__ __forceinline__ void schur_solve(BigShared<HM>& sh, int H, const doub
         const int lr = lane < K3 ? lane : 0;
         for (int j = 0; j + 1 < K3; ++j) {
             const double yj = bcast(x, j);
-            if (lane > j) x = fma(-sh.G[lr * LDG + j], yj, x);
+            if (lane > j) x = fma(-sh.G[gi(lr, j)], yj, x);
         }
         x *= sh.gid[lr];
         // backward: L^T q = y (lane r reads column r of L)
         for (int j = K3 - 1; j > 0; --j) {
             const double qj = bcast(x, j);
-            if (lane < j) x = fma(-sh.G[j * LDG + lr], qj, x);
+            if (lane < j) x = fma(-sh.G[gi(j, lr)], qj, x);
         }
         if (gv && lane < K3 && lane % 3 == 0) x -= cv[lane / 3];
         if (lane < K3) sh.q[lane] = x;
@@ -1360,7 +1383,9 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
 template <int HM, int MAXT, int FL>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT >= 512 ? KMPC_BIG_WPE : 1))) ipm_big(BigArgs A) {
     static_assert(3 * HM <= KP - 1, "Schur system must fit one wave");
-    __shared__ BigShared<HM> sh;
+    constexpr int NWB = MAXT / WAVE;
+    __shared__ double shraw[bs_doubles<HM>(NWB)];
+    BigShared<HM>& sh = *reinterpret_cast<BigShared<HM>*>(shraw);
     const SolveArgs& a = A.s;
     Win<HM, FL> W{a, sh, A.ws + (size_t)blockIdx.x * A.slab, a.N, a.H, A.NP, (int)(blockDim.x / WAVE),
                   (int)threadIdx.x, (int)threadIdx.x < a.N};
@@ -1371,7 +1396,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 #endif
     // fused solves on the >= 512-thread blocks (two per CU: the extra 13.6 KB fits; the 256-thread
     // blocks run three per CU at the LDS limit and keep the unfused sweeps)
-    __shared__ double fxs[(KMPC_BIG_FUSE && MAXT >= 512) ? fx_doubles<HM>() : 1];
+    __shared__ double fxs[(KMPC_BIG_FUSE && MAXT >= 512) ? fx_doubles<HM, NWB>() : 1];
     W.fx = (KMPC_BIG_FUSE && MAXT >= 512) ? fxs : nullptr;
     W.cs.set_case(!a.allow_short, (a.c > 0.0) || (a.tau > 0.0), a.tau > 0.0);
     const bool hw = W.hw(), hs = W.hs(), ht = W.ht();
