@@ -232,6 +232,26 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
                        const float* realized_next, double* weights, double* value, double* hist,
                        void* stream);
 
+/* A whole run_backtest per path in ONE launch (ABI 0.5.0): steps step0 .. step0 + n_steps - 1 of
+ * every path, each the kmpc_solve of that step's window then the kmpc_backtest_step bookkeeping,
+ * run back to back by one workgroup per path — no per-step launches, and no path waits for the
+ * slowest window of the step (the lock-step loop's bound at small P). The results are bit-identical
+ * to that loop (kmpc_solve of the P windows + kmpc_backtest_step per step): the same window solve
+ * and the same bookkeeping code.
+ *   sdesc:    the solve's program (B is ignored: the batch is desc->P; return_full_W must be 0).
+ *   yhat:     [n_steps, P, H, N] float32 forecasts of the steps (kmpc_rollout of their windows).
+ *   realized: [n_steps, P, N] float32 log-returns of each step's t + 1; steps k >= n_real have none
+ *             (realized_next = NULL in kmpc_backtest_step).
+ *   weights [P,N] f64, value [P] f64, hist [P,S,4]: as kmpc_backtest_step, updated in place.
+ *   target [P,N] f64, status [P] int, obj [P] f64: scratch (on return: the last step's W0, status,
+ *             objective).
+ * KMPC_ERR_UNSUPPORTED unless kmpc_solve would solve a batch of P such windows with the float64
+ * register kernel of the BASELINE C3 shape (H = 10, 64 < N < 104, no short, cost and cap, float64
+ * for this batch size); the caller then runs the lock-step loop. */
+int kmpc_backtest_run(const kmpc_backtest_desc* desc, const kmpc_solve_desc* sdesc, int step0, int n_steps,
+                      const float* yhat, const float* realized, int n_real, double* weights, double* value,
+                      double* hist, double* target, int* status, double* obj, void* stream);
+
 /* metrics [P,5]: Sharpe Ratio, Max Drawdown, Avg Turnover, Final Value, Total Return. */
 int kmpc_backtest_metrics(const kmpc_backtest_desc* desc, const double* hist, double* metrics,
                           void* stream);
@@ -294,7 +314,8 @@ const char* kmpc_strerror(int code);
    kmpc_rollout_desc.latent_unfused; 0.3.0 appended kmpc_solve_desc.precision and .mu_handoff:
    callers built against an older ABI must rebuild. 0.4.0 added enum values only
    (KMPC_PRECISION_MIXED, KMPC_DTYPE_F32_F32MFMA; AUTO precision now float64 below KMPC_MIXED_MIN_B
-   windows; KMPC_DTYPE_F32's GEMMs on three bf16 planes), no layout change. */
+   windows; KMPC_DTYPE_F32's GEMMs on three bf16 planes), no layout change. 0.5.0 added a function
+   (kmpc_backtest_run), no layout change. */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

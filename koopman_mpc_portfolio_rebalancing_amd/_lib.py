@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkmpc.so")
 
 KMPC_OK = 0
+KMPC_ERR_UNSUPPORTED = -2   # shape outside what the kernels were built for
 KMPC_MAX_LAYERS = 8
 KMPC_MAX_N = 1024
 KMPC_MAX_H = 21          # the Schur system (3H rows) is factored by one 64-lane wavefront
@@ -33,7 +34,7 @@ KMPC_MV_MAX_H = 16
 EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace_bytes",
                     "kmpc_backtest_step", "kmpc_backtest_metrics", "kmpc_standardize", "kmpc_strerror",
                     "kmpc_version", "kmpc_solve_mv", "kmpc_rolling_moments", "kmpc_solve_mv_ws",
-                    "kmpc_mv_workspace_bytes", "kmpc_gross_returns")
+                    "kmpc_mv_workspace_bytes", "kmpc_gross_returns", "kmpc_backtest_run")
 
 PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
 PRECISION_AUTO, PRECISION_F64, PRECISION_MIXED = 0, 1, 2   # kmpc_solve_desc.precision
@@ -42,8 +43,8 @@ MIXED_MIN_B = 2048   # KMPC_MIXED_MIN_B: AUTO runs the mixed pair from this many
 # ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
 # kmpc_rollout_desc.latent_unfused, 0.3.0 kmpc_solve_desc.precision and .mu_handoff, so an older
 # library would read them past its structs' end; 0.4.0 added enum values only (KMPC_PRECISION_MIXED,
-# KMPC_DTYPE_F32_F32MFMA), no layout change
-ABI_VERSION = "0.4.0"
+# KMPC_DTYPE_F32_F32MFMA), no layout change; 0.5.0 added kmpc_backtest_run
+ABI_VERSION = "0.5.0"
 
 
 class KmpcError(RuntimeError):
@@ -108,6 +109,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.kmpc_window.restype = ctypes.c_int
     L.kmpc_backtest_step.argtypes = [ctypes.POINTER(BacktestDesc), ctypes.c_int, vp, vp, vp, vp, vp, vp]
     L.kmpc_backtest_step.restype = ctypes.c_int
+    L.kmpc_backtest_run.argtypes = [ctypes.POINTER(BacktestDesc), ctypes.POINTER(SolveDesc), ctypes.c_int,
+                                    ctypes.c_int, vp, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp]
+    L.kmpc_backtest_run.restype = ctypes.c_int
     L.kmpc_backtest_metrics.argtypes = [ctypes.POINTER(BacktestDesc), vp, vp, vp]
     L.kmpc_backtest_metrics.restype = ctypes.c_int
     L.kmpc_standardize.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp]

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 from .koopman import DeviceKoopman, KoopmanModelSpec
-from .mpc import MPCConfig, solve_mpc_log_utility_batched
+from .mpc import MPCConfig, _solve_desc, solve_mpc_log_utility_batched
 
 
 @dataclass
@@ -220,7 +220,8 @@ LOCKSTEP_GROUPS_MAX_P = 1024
 
 def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: BacktestConfig,
                           mean, std, n_rows: Optional[int] = None, graph: bool = False,
-                          prerollout: bool = True, groups: Optional[int] = None) -> Dict[str, Any]:
+                          prerollout: bool = True, groups: Optional[int] = None,
+                          persistent: Optional[bool] = None) -> Dict[str, Any]:
     """P independent backtests of the reference loop (backtest.py:133-219) run in lock step on the
     device: at every step one batched window launch (kmpc_window over the P
     paths) and one bookkeeping launch (kmpc_backtest_step); calculate_metrics per path at the end
@@ -246,6 +247,12 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
             independent groups wait only for their own slowest path: the small-P backtest runs at
             the groups' mean step time instead of the maximum over all paths. Every window is
             solved by the same kernel as in one group, so the results are bit-identical.
+        persistent: run every step of a path in one launch (kmpc_backtest_run: one workgroup per
+            path, the step's solve then its bookkeeping, back to back) — no lock step at all, so a
+            path never waits for another path's window. Default: with prerollout, without graph or
+            groups, wherever the C ABI has the kernel for the shape (the C3 shape in float64: the
+            kernel kmpc_solve would use for the per-step batch); bit-identical to the lock-step
+            loop. Falls back to the loop where unsupported.
     Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
         reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
     """
@@ -274,12 +281,48 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
     H = int(strategy.mpc_config.horizon)
     sc = max(1, PREROLL_CHUNK // P)          # steps per batched rollout
     steps_t = torch.as_tensor(steps, dtype=torch.long, device=dev)
+    groups_arg = groups
     if groups is None:
         groups = LOCKSTEP_GROUPS if (prerollout and not graph and P <= LOCKSTEP_GROUPS_MAX_P) else 1
     groups = max(1, min(int(groups), P))
     if groups > 1 and (graph or not prerollout):
         raise ValueError("path groups need prerollout=True and graph=False")
     bounds = [(P * g) // groups for g in range(groups + 1)]
+    explicit = persistent
+    if persistent is None:
+        persistent = prerollout and not graph and groups_arg is None
+    if persistent and (graph or not prerollout):
+        raise ValueError("persistent needs prerollout=True and graph=False")
+
+    def run_persistent() -> bool:
+        """Every step of every path in kmpc_backtest_run launches (one per rollout chunk of sc steps):
+        False (nothing run) where the C ABI has no persistent kernel for this shape."""
+        sdesc = _solve_desc(P, N, H, strategy.mpc_config, False)
+        target = torch.empty((P, N), dtype=torch.float64, device=dev)
+        status = torch.empty((P,), dtype=torch.int32, device=dev)
+        objv = torch.empty((P,), dtype=torch.float64, device=dev)
+        sh = _lib.stream_handle(dev)
+
+        def call(k0, n, y, rr, n_real):
+            return L.kmpc_backtest_run(ctypes.byref(d), ctypes.byref(sdesc), k0, n, y, rr, n_real, w.data_ptr(),
+                                       value.data_ptr(), hist.data_ptr(), target.data_ptr(), status.data_ptr(),
+                                       objv.data_ptr(), sh)
+
+        rc = call(0, 0, None, None, 0)   # (shape check only)
+        if rc == _lib.KMPC_ERR_UNSUPPORTED:
+            if explicit:
+                raise ValueError("persistent=True: no persistent backtest kernel for this shape")
+            return False
+        _lib.check(rc)
+        for k0 in range(0, S, sc):
+            n = min(sc, S - k0)
+            y = km.rollout(xt[steps_t[k0:k0 + n]].reshape(n * P, -1), m, sd, H, N).contiguous()
+            tn = steps_t[k0:k0 + n] + 1
+            n_real = int((tn < T).sum().item())   # (steps increase: the rows with a t + 1 are a prefix)
+            rr = rt[tn[:n_real]].contiguous() if n_real else None
+            _lib.check(call(k0, n, y.data_ptr(), rr.data_ptr() if rr is not None else None, n_real))
+        _lib.check(L.kmpc_backtest_metrics(ctypes.byref(d), hist.data_ptr(), metrics.data_ptr(), sh))
+        return True
 
     def run_steps():
         y = None
@@ -333,7 +376,9 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
                                                _lib.stream_handle(dev)))
 
     with torch.cuda.device(dev):
-        if groups > 1 and S:
+        if persistent and S and run_persistent():
+            pass
+        elif groups > 1 and S:
             run_groups()
         elif graph and S:
             g = torch.cuda.CUDAGraph()

@@ -16,7 +16,7 @@ LIB = os.path.join(HERE, "libkmpc.so")
 
 def sources():
     return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))
-            if f.endswith((".hip", ".h", "Makefile"))] + [os.path.join(os.path.dirname(HERE), "include", "kmpc.h")]
+            if f.endswith((".hip", ".h", ".inc", "Makefile"))] + [os.path.join(os.path.dirname(HERE), "include", "kmpc.h")]
 
 
 def is_stale() -> bool:

@@ -26,7 +26,7 @@ int check_solve(const kmpc_solve_desc* d) {
 
 extern "C" {
 
-const char* kmpc_version(void) { return "kmpc 0.4.0 (gfx950)"; }
+const char* kmpc_version(void) { return "kmpc 0.5.0 (gfx950)"; }
 
 const char* kmpc_strerror(int code) {
     switch (code) {
@@ -118,6 +118,23 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
     if (desc->P > 0 && (!target || !weights || !value || !hist)) return KMPC_ERR_INVALID;
     return kmpc::backtest_step_launch(desc, step, target, realized_next, weights, value, hist,
                                       (hipStream_t)stream);
+}
+
+int kmpc_backtest_run(const kmpc_backtest_desc* desc, const kmpc_solve_desc* sdesc, int step0, int n_steps,
+                      const float* yhat, const float* realized, int n_real, double* weights, double* value,
+                      double* hist, double* target, int* status, double* obj, void* stream) {
+    if (!desc || !sdesc || desc->P < 0 || desc->N < 1 || desc->S < 1 || step0 < 0 || n_steps < 0 ||
+        step0 + n_steps > desc->S || n_real < 0 || n_real > n_steps || sdesc->N != desc->N)
+        return KMPC_ERR_INVALID;
+    kmpc_solve_desc sd = *sdesc;   // (the batch is the paths)
+    sd.B = desc->P;
+    const int rc = check_solve(&sd);
+    if (rc) return rc;
+    if (desc->P > 0 && n_steps > 0 &&
+        (!yhat || !weights || !value || !hist || !target || !status || !obj || (n_real > 0 && !realized)))
+        return KMPC_ERR_INVALID;
+    return kmpc::backtest_run_launch(desc, &sd, step0, n_steps, yhat, realized, n_real, weights, value, hist,
+                                     target, status, obj, (hipStream_t)stream);
 }
 
 int kmpc_standardize(int T, int N, const double* log_returns, const double* mean, const double* std,

@@ -12,6 +12,10 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
                  int* status, double* obj, int* iters, void* ws, size_t ws_bytes, hipStream_t stream,
                  double* trace = nullptr);
 
+int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd, int step0, int n_steps,
+                        const float* yhat, const float* realized, int n_real, double* weights, double* value,
+                        double* hist, double* target, int* status, double* obj, hipStream_t stream);
+
 // kmpc_backtest.hip
 int gross_returns_launch(size_t n, const float* yhat, float* R, hipStream_t stream);
 int backtest_step_launch(const kmpc_backtest_desc* d, int step, const double* target,

@@ -357,4 +357,26 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     return KMPC_ERR_UNSUPPORTED;   // H > 10: the large-window kernel
 }
 
+// kmpc_backtest_run: the path-persistent kernel exists for the shape whose per-step batch of P
+// windows kmpc_solve sends to the float64 C3 kernel (ipm_kernel<10, 128, true, 7, QL_CS, true>):
+// H = 10, 64 < N < QL_CS, no short, cost and cap, float64 for this batch (not mixed_case)
+int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd, int step0, int n_steps,
+                        const float* yhat, const float* realized, int n_real, double* weights, double* value,
+                        double* hist, double* target, int* status, double* obj, hipStream_t stream) {
+    kmpc_solve_desc d = *sd;
+    d.B = bd->P;
+    SolveArgs a = make_args(&d);
+    const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
+    if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || !fl7 || a.H != 10 || a.N <= 64 ||
+        a.N >= QL_CS)
+        return KMPC_ERR_UNSUPPORTED;
+    if (a.path != KMPC_PATH_AUTO && a.path != KMPC_PATH_REGISTER && a.path != KMPC_PATH_REGISTER_UNPACKED)
+        return KMPC_ERR_UNSUPPORTED;
+    if (bd->P == 0 || n_steps == 0) return KMPC_OK;
+    a.wout = target; a.status = status; a.obj = obj; a.iters = nullptr; a.trace = nullptr;
+    a.yhat = yhat; a.wp = weights;
+    return launch_bt_run_c3(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value,
+                            hist, stream);
+}
+
 }  // namespace kmpc

@@ -34,6 +34,8 @@ __host__ __device__ inline size_t warm_stride(int H, int N) {
     return ((size_t)WARM_HEAD + 5 * (size_t)H * N + 3 * (size_t)H + 15) / 16 * 16;
 }
 
+constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
+
 // ipm_kernel launchers, one translation unit per compile-time horizon bound HM (kmpc_solve_h*.hip)
 template <int HM>
 int launch_ipm(const SolveArgs& a, hipStream_t stream);
@@ -45,6 +47,10 @@ template <int HM>
 int launch_ipm_case(const SolveArgs& a, hipStream_t stream);
 // the C3 kernel (H = 10, FL = 7, 128 threads, LDL^T arrays in LDS) in its own -O2 unit (kmpc_solve_c3.hip)
 int launch_ipm_c3(const SolveArgs& a, hipStream_t stream);
+// the path-persistent backtest kernel of the C3 shape (kmpc_solve_c3.hip): a.B = paths, a.wout the
+// [P, N] W0 scratch, a.status / a.obj [P] scratch; n_steps steps from history row step0
+int launch_bt_run_c3(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
+                     int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream);
 // packed small-window kernels, 64 / GL windows per wave (kmpc_solve_p*.hip); KMPC_ERR_UNSUPPORTED
 // outside N <= 32, 3 H <= 32
 template <int HM>

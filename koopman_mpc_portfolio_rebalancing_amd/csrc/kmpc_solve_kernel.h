@@ -1736,436 +1736,7 @@ __attribute__((amdgpu_waves_per_eu(PH == 1 ? KMPC_F32_WPE : (HM <= KMPC_WPE2_HM 
     auto& sh = shv[grp<GL>()];
     const int b = blockIdx.x * WPB + grp<GL>();
     if (b >= args.B) return;   // (whole groups of the last block)
-    if constexpr (PH == 3) {   // the retry pass: only windows whose warm start did not end optimal
-        if (reinterpret_cast<const int*>(args.warm + (size_t)b * warm_stride(args.H, args.N))[0] != 3) return;
-    }
-    // waves in the block: a compile-time constant up to 128 threads (the launchers use MAXT = 128
-    // only for 128-thread blocks), so the reductions' per-wave slot loops need no run-time guards
-    const int nw = GL < 64 ? 1 : (MAXT <= 128 ? NWM : (int)(blockDim.x / WAVE));
-    Reducer<HM, NWM, GL, Real> R(sh, nw);
-    Thread<HM, MAXT, FL, CS, QL, GL, Real> T;
-    T.bind_cold();
-    T.H = EXACT ? HM : args.H;
-    T.N = args.N;
-    T.i = gvt<GL>();
-    T.act = T.i < args.N;
-    T.set_case(!args.allow_short, (args.c > Real(0.0)) || (args.tau > Real(0.0)), args.tau > Real(0.0));
-    T.tau = args.tau;
-    const int H = T.H, N = T.N;
-    const double* wp = args.wp + (size_t)b * N;   // (H is a compile-time constant when EXACT)
-    const float* yh = args.yhat + (size_t)b * H * N;
-    T.wpi = T.act ? wp[T.i] : Real(0.0);
-
-    // ---- inputs: m = R - 1 with R = np.exp(yhat) in float32 (mpc.py:55), objective scale,
-    //      finiteness (a non-finite yhat or an overflowing R -> solver_error) ----
-    Real mx = Real(0.0);
-    bool finite = true;
-    bool r_zero = false;
-    {
-        Real rs[HM];   // per period S_t = sum_i R_t,i of the float32 R
-#pragma unroll
-        for (int t = 0; t < HM; ++t) {
-            T.m[t] = rs[t] = Real(0.0);
-            if (T.act && t < H) {
-                const float r = np_expf(yh[t * N + T.i]);
-                T.m[t] = (Real)((double)r - 1.0);
-                rs[t] = (Real)r;
-                finite = finite && isfinite(T.m[t]);
-            }
-        }
-        if (T.act) finite = finite && isfinite(T.wpi);
-        R.periods(rs);
-        // S_t = 0 (every R underflowed, yhat <= -103.97): R_t . w_t = 0 on the whole simplex and the
-        // reference's exp cone exp(u) <= R_t . w_t has no solution — cvxpy reports infeasible.
-        // 0 < S_t < TINY_PERIOD (every yhat below ~ -11): the program is the same for R_t / S_t up to
-        // the constant log S_t, and m = R - 1 would round to -1 (R below 2^-53), so that period runs
-        // on m = R / S_t - 1 and the objective adds log S_t back (sh.lsc; oracle: kmpc_oracle_solve)
-#pragma unroll
-        for (int t = 0; t < HM; ++t) {
-            r_zero = r_zero || (t < H && rs[t] == Real(0.0));
-            if (T.act && t < H && rs[t] > Real(0.0) && rs[t] < Real(TINY_PERIOD))
-                T.m[t] = (Real)((double)np_expf(yh[t * N + T.i]) / (double)rs[t] - 1.0);
-            if (T.act && t < H) mx = fmax(mx, fabs(T.m[t]));
-        }
-        if (gvt<GL>() == 0) {
-#pragma unroll
-            for (int t = 0; t < HM; ++t)
-                sh.lsc[t] = (t < H && rs[t] > Real(0.0) && rs[t] < Real(TINY_PERIOD)) ? (Real)log((double)rs[t]) : Real(0.0);
-        }
-    }
-    mx = R.max1(mx);
-    const Real nonfinite = R.max1(finite ? Real(0.0) : Real(1.0));
-    Real sig = fmax(mx, Real(args.c));
-    if (!(sig > Real(0.0))) sig = Real(1.0);
-    T.sig = sig;
-    T.isig = Real(1.0) / sig;
-    T.irsig = Real(1.0) / sqrt(sig);
-    T.c = Real(args.c) / sig;
-
-    int status = KMPC_STATUS_SOLVER_ERROR;
-    int it = 0;
-    double* wout = args.wout + (size_t)b * (args.return_full ? H * N : N);
-    const int tw = args.return_full ? H : 1;   // periods written out
-    double best_obj = __builtin_nan("");
-    bool handoff = false;   // PH = 1: the iterate went to the window's warm record
-    int it0 = 0;            // PH >= 2: iterations of the earlier phases (reported with these)
-
-    if (nonfinite == Real(0.0) && isfinite(args.c) && isfinite(args.tau)) {
-        if (r_zero) {
-            status = KMPC_STATUS_INFEASIBLE;
-        } else if (args.allow_short && !T.hs) {
-            // no bounds and no turnover terms: unbounded unless every period is flat
-            Real msum[HM];
-#pragma unroll
-            for (int t = 0; t < HM; ++t) msum[t] = (T.act && t < H) ? T.m[t] : Real(0.0);
-            R.periods(msum);
-            Real spread = Real(0.0);
-#pragma unroll
-            for (int t = 0; t < HM; ++t)
-                if (T.act && t < H) spread = fmax(spread, fabs(T.m[t] - msum[t] / N));
-            spread = R.max1(spread);
-            if (spread == Real(0.0)) {
-                const Real swp = R.sum1(T.act ? T.wpi : Real(0.0));
-#pragma unroll
-                for (int t = 0; t < HM; ++t) T.w[t] = swp != Real(0.0) ? T.wpi / swp : Real(1.0) / N;
-                if constexpr (PH != 1) best_obj = record_best<HM, NWM>(T, R, wout, yh, args.c, tw);
-                status = KMPC_STATUS_OPTIMAL;
-            } else {
-                status = KMPC_STATUS_UNBOUNDED;
-            }
-        } else {
-            // ---- initial point: the float32 phase's iterate (PH = 2, warm window), else the
-            //      usual one ----
-            bool warm = false;
-            const float* rec = nullptr;
-            if constexpr (PH == 2) {
-                rec = args.warm + (size_t)b * warm_stride(H, N);
-                // (a wave-uniform flag: a scalar branch; unchanged in memory until the end)
-                warm = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int*>(rec)[0]) == 1;
-            }
-            if (warm) {
-                const float* st = rec + WARM_HEAD;
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    const bool on = T.act && t < H;
-                    const int k = t * N + T.i;
-                    T.w[t] = on ? (Real)st[k] : Real(0.0);
-                    T.s[t] = on ? (Real)st[H * N + k] : Real(0.0);
-                    T.l1[t] = on ? (Real)st[2 * H * N + k] : Real(0.0);
-                    T.l2[t] = on ? (Real)st[3 * H * N + k] : Real(0.0);
-                    T.l3[t] = on ? (Real)st[4 * H * N + k] : Real(0.0);
-                }
-                if (gvt<GL>() < HM) {
-                    const int t = gvt<GL>();
-                    const bool on = t < H;
-                    sh.z4[t] = on ? (Real)st[5 * H * N + t] : Real(1.0);
-                    sh.l4[t] = on ? (Real)st[5 * H * N + H + t] : Real(0.0);
-                    sh.nu[t] = on ? (Real)st[5 * H * N + 2 * H + t] : Real(0.0);
-                }
-            } else {
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    const Real b0 = T.hw ? fmax(T.wpi, Real(0.0)) : T.wpi;
-                    T.w[t] = (T.act && t < H) ? Real(0.5) * b0 + Real(0.5) / N : Real(0.0);
-                }
-                Real ss0[HM];
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    const bool on = T.act && t < H;
-                    const Real d = T.w[t] - T.wprev(t);
-                    T.s[t] = (on && T.hs) ? fabs(d) + Real(1.0) / N : Real(0.0);
-                    ss0[t] = T.s[t];
-                    T.l1[t] = (on && T.hw) ? Real(1.0) : Real(0.0);
-                    T.l2[t] = T.l3[t] = (on && T.hs) ? Real(1.0) : Real(0.0);
-                }
-                const Real st0 = R.own1(ss0);
-                if (gvt<GL>() < HM) {
-                    const int t = gvt<GL>();
-                    const Real st = st0;
-                    sh.z4[t] = (T.ht && t < H) ? fmax(T.tau - st, Real(0.5) * T.tau) : Real(1.0);
-                    sh.l4[t] = (T.ht && t < H) ? Real(1.0) : Real(0.0);
-                    sh.nu[t] = Real(0.0);
-                }
-            }
-            __syncthreads();
-            const int ncon = (T.hw ? H * N : 0) + (T.hs ? 2 * H * N : 0) + (T.ht ? H : 0);
-            const Real inv_ncon = Real(1.0) / (ncon > 0 ? ncon : 1);
-            Real best = huge_of<Real>(), min_pr = huge_of<Real>();
-            Real last_mu = huge_of<Real>();   // PH = 1: stagnation test
-
-            PhaseClock ph;
-            KMPC_PH_START(ph);
-            for (it = 0; it < args.max_iter; ++it) {
-                // ---- residuals: den_t = 1 + m.w, 1'w_t - 1, tau - 1's_t - z4 ----
-                Real my_rw = Real(0.0);   // this period thread's R.w total
-                Real own_rc4 = Real(0.0), own_pr = Real(0.0);   // this period thread's z4 l4, max(|rp|, |rg4|)
-                bool own_bad = false;                 // ... and R.w <= 0
-                Real l1_own[HM];    // this asset's |w_t - w_{t-1}|, reduced only when the iterate is kept
-                {
-                    Real mw[HM], sw[HM], ssum[HM], l1n[HM];
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) {
-                        const bool on = t < H;   // (inactive lanes: zero iterate)
-                        mw[t] = on ? T.m[t] * T.w[t] : Real(0.0);
-                        sw[t] = on ? T.w[t] : Real(0.0);
-                        ssum[t] = on ? T.s[t] : Real(0.0);
-                        l1n[t] = on ? fabs(T.w[t] - T.wprev(t)) : Real(0.0);
-                    }
-                    // (folding l1n into this reduction as a fourth array is slower: the 64-slot
-                    // reduce-scatter costs more than the separate one-barrier own1 below)
-                    Real o[4];
-                    R.own3(mw, sw, ssum, o);
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) l1_own[t] = l1n[t];
-                    if (gvt<GL>() < HM) {
-                        const int t = gvt<GL>();
-                        const Real a = o[0], b2 = o[1], c2 = o[2];
-                        my_rw = b2 + a;          // sum_i exp(yhat) w = sum w + sum expm1(yhat) w
-                        const bool on = t < H;
-                        sh.den[t] = Real(1.0) + a;
-                        sh.iden[t] = Real(1.0) / (Real(1.0) + a);
-                        sh.rp[t] = on ? b2 - Real(1.0) : Real(0.0);
-                        sh.rg4[t] = (T.ht && on) ? T.tau - c2 - sh.z4[t] : Real(0.0);
-                        sh.rc4[t] = (T.ht && on) ? sh.z4[t] * sh.l4[t] : Real(0.0);
-                        sh.iz4[t] = Real(1.0) / sh.z4[t];
-                        if (on) {
-                            own_rc4 = sh.rc4[t];
-                            own_pr = fmax(fabs(sh.rp[t]), fabs(sh.rg4[t]));
-                            own_bad = !(sh.den[t] > Real(0.0));
-                        }
-                        newton_rows<HM, NWM>(T, sh, t);   // the predictor's rows
-                    }
-                    __syncthreads();
-                }
-                Real mu_l = Real(0.0), rd = Real(0.0);
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    if (t < H) {
-                        const Real d = T.w[t] - T.wprev(t);
-                        Real rdw, rds;
-                        dual_residual<HM, NWM>(T, sh, t, rdw, rds);
-                        mu_l += (T.hw ? T.w[t] * T.l1[t] : Real(0.0)) +
-                                (T.hs ? (T.s[t] - d) * T.l2[t] + (T.s[t] + d) * T.l3[t] : Real(0.0));
-                        rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
-                    }
-                }
-                if (!T.act) rd = Real(0.0);   // (an inactive lane's mu terms are zero; its dual rows are not rows)
-                // the period owners' cap complementarity, primal residual and domain check ride
-                // along in the same reduction (a domain failure as an infinite dual residual: the
-                // merit is then non-finite and the loop stops, as before)
-                Real mu, pr;
-                R.sum_max2(mu_l + own_rc4, own_bad ? Real(__builtin_inf()) : rd, own_pr, mu, rd, pr);
-                const Real mu_sum = mu;   // c0 of the complementarity polynomial (cap terms included)
-                const bool domain_ok = true;
-                mu *= inv_ncon;
-                const Real merit = fmax(mu, fmax(rd, pr));
-                min_pr = fmin(min_pr, pr);
-                if (PH != 1 && args.trace && b == 0 && gvt<GL>() == 0) {
-                    args.trace[4 * it + 0] = mu; args.trace[4 * it + 1] = rd; args.trace[4 * it + 2] = pr;
-                }
-                if (!domain_ok || !isfinite(merit)) break;
-                if constexpr (PH == 1) {
-                    // float32 phase: hand the iterate over once mu <= mu_handoff (measured on the
-                    // oracle, tools/f32phase_probe.py), or when float32 stops making progress
-                    if (mu <= Real(args.mu_handoff) || (it > 3 && mu > Real(0.9) * last_mu)) {
-                        handoff = true;
-                        break;
-                    }
-                    last_mu = mu;
-                } else if (merit < best) {
-                    best = merit;
-                    // the answer is this iterate: W to HBM, its period totals for problem.value
-                    // (evaluated once, after the loop)
-#pragma unroll
-                    for (int t = 0; t < HM; ++t)
-                        if (T.act && t < H && t < tw) wout[t * N + T.i] = T.w[t];
-                    const Real l1t = R.own1(l1_own);
-                    if (gvt<GL>() < HM) {
-                        sh.best_rw[gvt<GL>()] = my_rw;
-                        sh.best_l1[gvt<GL>()] = l1t;
-                    }
-                    best_obj = Real(0.0);
-                } else {
-                    if (best < Real(1e-6) && merit > Real(1e4) * best)
-                        break;   // numerical breakdown after convergence: keep the best iterate
-                }
-                if (PH != 1 && mu < args.tol && rd < Real(10.0) * args.tol && pr < Real(10.0) * args.tol) break;
-                KMPC_PH(ph, 0);
-                if (!factor<HM, NWM>(T, sh, R, ph)) break;
-                // the predictor's targets rc = x l (read by its multipliers; its solve folds them into
-                // the right-hand side, newton())
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    Real r1 = Real(0.0), r2 = Real(0.0), r3 = Real(0.0);
-                    if (t < H) T.xl(t, r1, r2, r3);   // (inactive lanes: zero)
-                    T.rc1.set(t, r1);
-                    T.rc2.set(t, r2);
-                    T.rc3.set(t, r3);
-                }
-
-                // ---- predictor (pass 0) and corrector (pass 1) share one Newton body ----
-                Real step = Real(0.0);
-                for (int pass = 0; pass < 2; ++pass) {
-                    // predictor unrefined (it only sets the step estimate, sigma and the
-                    // second-order term); corrector refined adaptively once mu <= REFINE_MU (_SHORT)
-                    // (before that G is well conditioned and the IPM self-corrects) — as the oracle
-                    // w and s are not read by the Newton solve: park them in scratch across it
-                    // (plain stores; one batch of loads after), so that their 40 VGPRs serve the
-                    // solve. Left to itself the register allocator spills other state instead and
-                    // reloads it piecemeal inside the iteration (107 -> 54 spilled dwords; C3 solve
-                    // +6%, N = 250 +16%, measured r02). The empty asm takes the array's address,
-                    // so it stays in memory and the loads are not forwarded from the stores.
-                    // (the float32 phase has registers to spare at one wave per SIMD: no parking
-                    // unless KMPC_F32_PARK)
-                    constexpr bool PARK = sizeof(Real) == 8 ? KMPC_F64_PARK : KMPC_F32_PARK;
-                    Real park[2 * HM];
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) { park[t] = T.w[t]; park[HM + t] = T.s[t]; }
-                    if constexpr (PARK) asm volatile("" :: "v"(&park[0]) : "memory");
-                    newton<HM, NWM>(T, sh, R, (PH == 1 || pass == 0 || mu > (T.hw ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : args.n_refine,
-                                    pass == 0);
-                    if constexpr (PARK) asm volatile("" :: "v"(&park[0]) : "memory");
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) { T.w[t] = park[t]; T.s[t] = park[HM + t]; }
-                    KMPC_PH(ph, 4);
-                    Real cc1, cc2;
-                    const Real amax = max_step<HM, NWM>(T, sh, R, cc1, cc2);
-                    if (pass == 1) { step = fmin(Real(1.0), Real(0.99) * amax); break; }
-                    const Real ap = fmin(Real(1.0), amax);
-                    const Real comp = mu_sum + ap * (cc1 + ap * cc2);   // (cap terms in cc1, cc2: max_step)
-                    Real sg = comp * inv_ncon / mu;
-                    sg = sg * sg * sg;
-                    const Real smu = sg * mu;
-                    Real DL1[HM], DL2[HM], DL3[HM];
-                    T.dual_dirs_all(DL1, DL2, DL3);
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) {
-                        // the corrector's targets x l + dx_aff dl_aff - sigma mu (inactive lanes:
-                        // -smu, multiplied by zero reciprocals wherever read)
-                        Real r1 = Real(0.0), r2 = Real(0.0), r3 = Real(0.0);
-                        if (t < H) {
-                            const Real dl1 = DL1[t], dl2 = DL2[t], dl3 = DL3[t];
-                            const Real dd = T.dw[t] - (t ? T.dw[t - 1] : Real(0.0));
-                            r1 = T.rc1[t]; r2 = T.rc2[t]; r3 = T.rc3[t];
-                            r1 += T.dw[t] * dl1 - smu;
-                            r2 += (T.ds[t] - dd) * dl2 - smu;
-                            r3 += (T.ds[t] + dd) * dl3 - smu;
-                        }
-                        if (T.hw) T.rc1.set(t, r1);
-                        if (T.hs) {
-                            T.rc2.set(t, r2);
-                            T.rc3.set(t, r3);
-                        }
-                    }
-                    if (gvt<GL>() < HM && T.ht && (int)gvt<GL>() < H) {
-                        const int t = gvt<GL>();
-                        sh.rc4[t] += sh.dz4[t] * sh.dl4[t] - smu;
-                    }
-                    if (gvt<GL>() < HM) newton_rows<HM, NWM>(T, sh, gvt<GL>());   // the corrector's rows
-                    __syncthreads();
-                }
-                if (PH != 1 && args.trace && b == 0 && gvt<GL>() == 0) args.trace[4 * it + 3] = step;
-                KMPC_PH(ph, 5);
-                // ---- update ----
-                {
-                    Real DL1[HM], DL2[HM], DL3[HM];
-                    T.dual_dirs_all(DL1, DL2, DL3);
-#pragma unroll
-                    for (int t = 0; t < HM; ++t) {
-                        if (t < H) {   // (inactive lanes: zero direction)
-                            T.l1[t] += step * DL1[t];
-                            T.l2[t] += step * DL2[t];
-                            T.l3[t] += step * DL3[t];
-                        }
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < HM; ++t) {
-                    if (t < H) {
-                        T.w[t] += step * T.dw[t];
-                        T.s[t] += step * T.ds[t];
-                    }
-                }
-                // every thread's max_step ratio test (pass 1) has read sh.z4 / sh.l4 before the
-                // period threads overwrite them; the next reads (period owners, then everyone) sit
-                // behind the next iteration's residual barriers
-                __syncthreads();
-                if (gvt<GL>() < HM && (int)gvt<GL>() < H) {
-                    const int t = gvt<GL>();
-                    sh.z4[t] += step * sh.dz4[t];
-                    sh.l4[t] += step * sh.dl4[t];
-                    sh.nu[t] += step * sh.dnu[t];
-                }
-                KMPC_PH(ph, 6);
-            }
-            __syncthreads();   // sh.best_* of the best iterate visible
-            if (PH != 1 && best < huge_of<Real>()) {
-                // problem.value (mpc.py:103) at the best iterate: sum_t log(R_t . w_t) - c ||w_t - w_{t-1}||_1
-                Real f = Real(0.0);
-                for (int t = 0; t < H; ++t) f += log(sh.best_rw[t]) + sh.lsc[t] - args.c * sh.best_l1[t];
-                best_obj = f;
-            }
-            if (best <= Real(1e-7)) status = KMPC_STATUS_OPTIMAL;
-            else if (best <= Real(1e-4)) status = KMPC_STATUS_OPTIMAL_INACCURATE;
-            else if (min_pr > Real(1e-6)) status = KMPC_STATUS_INFEASIBLE;   // primal residual never closed
-            else status = KMPC_STATUS_SOLVER_ERROR;
-        }
-    }
-    if constexpr (PH == 1) {
-        // the window's warm record: the iterate at the handoff (float32, [5][H][N] + [3][H]),
-        // or a cold mark (special cases, a float breakdown: the float64 phase starts over)
-        float* rec = args.warm + (size_t)b * warm_stride(H, N);
-        if (handoff) {
-            float* st = rec + WARM_HEAD;
-#pragma unroll
-            for (int t = 0; t < HM; ++t) {
-                if (T.act && t < H) {
-                    const int k = t * N + T.i;
-                    st[k] = T.w[t];
-                    st[H * N + k] = T.s[t];
-                    st[2 * H * N + k] = T.l1[t];
-                    st[3 * H * N + k] = T.l2[t];
-                    st[4 * H * N + k] = T.l3[t];
-                }
-            }
-            if (gvt<GL>() < H) {
-                const int t = gvt<GL>();
-                st[5 * H * N + t] = sh.z4[t];
-                st[5 * H * N + H + t] = sh.l4[t];
-                st[5 * H * N + 2 * H + t] = sh.nu[t];
-            }
-        }
-        if (gvt<GL>() == 0) {
-            int* hd = reinterpret_cast<int*>(rec);
-            hd[0] = handoff ? 1 : 0;
-            hd[1] = it;
-        }
-        return;
-    }
-    __syncthreads();
-    // ---- outputs: W was written by record_best; fallback (mpc.py:113-115) otherwise ----
-    const bool ok = status == KMPC_STATUS_OPTIMAL || status == KMPC_STATUS_OPTIMAL_INACCURATE;
-    if (!ok && T.act) {
-#pragma unroll
-        for (int t = 0; t < HM; ++t)
-            if (t < tw) wout[t * N + T.i] = T.wpi;
-    }
-    if (gvt<GL>() == 0) {
-        args.obj[b] = ok ? best_obj : __builtin_nan("");
-        args.status[b] = status;
-        if constexpr (PH >= 2) {   // + the earlier phases' iterations (spent on a cold window too)
-            int* hd = reinterpret_cast<int*>(args.warm + (size_t)b * warm_stride(H, N));
-            it0 = hd[1];
-            // a warm start (header flag 1, re-read here rather than kept live across the loop)
-            // that did not end optimal: the retry pass (PH = 3) solves the window again from the
-            // usual initial point, so no status is worse than the float64-only one
-            if (PH == 2 && hd[0] == 1 && status != KMPC_STATUS_OPTIMAL) {
-                hd[0] = 3;
-                hd[1] = it + it0;
-            }
-        }
-        if (args.iters) args.iters[b] = it + it0;
-    }
+#include "kmpc_ipm_body.inc"
 }
 
 template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false, int GL = 64, int PH = 0>
@@ -2176,7 +1747,6 @@ int launch_one(const SolveArgs& a, int nt, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
 }
 
-constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
 constexpr int QL_CS256 = 216;  // ... and of the 256-thread one
 
 // Generic launcher (constraint case read at run time): one workgroup of 64 * ceil(N / 64) threads

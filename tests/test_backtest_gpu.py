@@ -195,3 +195,55 @@ def test_lockstep_path_groups_on_streams_equal_one_group(P, groups):
         assert torch.equal(one[k], grp[k]), k
     for k, v in one["metrics"].items():
         assert torch.equal(v, grp["metrics"][k]), k
+
+
+@pytest.mark.parametrize("P,T,chunk", [(64, 22, None), (61, 19, 128)])
+def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, monkeypatch):
+    """run_backtest_lockstep(persistent=True): every step of every path in kmpc_backtest_run launches
+    (one workgroup per path: the step's solve, then its bookkeeping, back to back) against the
+    lock-step loop (one kmpc_solve over the P windows + one kmpc_backtest_step per step): the same
+    window solve and bookkeeping code, so histories, weights and metrics are bit-identical. P = 61
+    with 2 steps per rollout chunk: several launches, each resuming the paths' state."""
+    import bench
+    from koopman_mpc_portfolio_rebalancing_amd import backtest as bt
+    dev = torch.device("cuda")
+    N, L, H = 100, 256, 10
+    obs_n = N * 20
+    spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(P, T, obs_n, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    if chunk:
+        monkeypatch.setattr(bt, "PREROLL_CHUNK", chunk)
+    loop = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False, groups=1)
+    per = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=True)
+    assert per["return"].shape == (P, T - H)
+    for k in ("portfolio_value", "return", "turnover", "cost", "weights"):
+        assert torch.equal(loop[k], per[k]), k
+    for k, v in loop["metrics"].items():
+        assert torch.equal(v, per["metrics"][k]), k
+    assert run_backtest_lockstep(strat, x, r, cfg, mean, std)["portfolio_value"].equal(per["portfolio_value"])
+
+
+def test_persistent_backtest_unsupported_shape():
+    """persistent=True on a shape without a persistent kernel (H = 5) raises; the default falls back
+    to the lock-step loop."""
+    import bench
+    dev = torch.device("cuda")
+    N, L, H, P, T = 100, 256, 5, 8, 9
+    obs_n = N * 20
+    spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(P, T, obs_n, generator=g).to(dev)
+    r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)
+    mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
+    cfg = BacktestConfig(horizon=H)
+    with pytest.raises(ValueError):
+        run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=True)
+    a = run_backtest_lockstep(strat, x, r, cfg, mean, std)
+    b = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False, groups=1)
+    assert torch.equal(a["portfolio_value"], b["portfolio_value"])

@@ -68,6 +68,21 @@ def test_argument_errors_need_no_gpu():
     assert lib.kmpc_backtest_step(ctypes.byref(bt), 4, None, None, None, None, None, None) == -1   # step >= S
     assert lib.kmpc_backtest_step(ctypes.byref(bt), 0, None, None, None, None, None, None) == -1   # null arrays
     assert lib.kmpc_backtest_metrics(None, None, None, None) == -1
+    # kmpc_backtest_run: argument checks, then the shape check (n_steps = 0: no launch)
+    sd = _lib.SolveDesc()
+    sd.B, sd.N, sd.H, sd.cost_coeff, sd.max_turnover = 0, 100, 10, 1e-3, 0.2
+    btr = _lib.BacktestDesc(64, 100, 20, 1e-3)
+    run = lambda *a: lib.kmpc_backtest_run(ctypes.byref(btr), ctypes.byref(sd), *a, *([None] * 6), None)
+    assert run(0, 0, None, None, 0) == 0                      # the C3 shape in float64: supported
+    assert run(15, 6, None, None, 0) == -1                    # past the history's S rows
+    assert run(0, 2, None, None, 0) == -1                     # null arrays
+    assert run(0, 0, None, None, 1) == -1                     # more realized rows than steps
+    sd.precision = 2                                          # MIXED: the per-step batch runs the pair
+    assert run(0, 0, None, None, 0) == -2
+    sd.precision, sd.H = 0, 5                                 # another horizon: no persistent kernel
+    assert run(0, 0, None, None, 0) == -2
+    sd.H, sd.cost_coeff = 10, -1.0                            # the solve's own checks apply
+    assert run(0, 0, None, None, 0) == -1
     bt.P = 0
     assert lib.kmpc_backtest_metrics(ctypes.byref(bt), None, None, None) == 0
     mv = _lib.MvDesc()
