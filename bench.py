@@ -455,10 +455,12 @@ def secondary_c1(dev, steps: int, warmup: int, B: int = 65536) -> dict:
 
 
 def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
-    """SURVEY §8(f) row 1 at a small path count: P lock-stepped backtest paths
-    of the headline model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2) over T test rows,
-    run_backtest_lockstep with its defaults (forecasts rolled out up front, path groups on streams);
-    path-steps/s = P x steps / wall time of the second of two identical runs."""
+    """SURVEY §8(f) row 1 at a small path count: P backtest paths of the
+    headline model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2) over T test rows,
+    run_backtest_lockstep with its defaults (forecasts rolled out up front, then every step of every
+    path in one path-persistent launch, kmpc_backtest_run; bit-identical to the lock-step loop);
+    path-steps/s = P x steps / wall time of the second of two identical runs. Beside it the
+    lock-step loop (three path groups on streams) for comparison."""
     from koopman_mpc_portfolio_rebalancing_amd import BacktestConfig, KoopmanModelSpec, KoopmanMPCStrategy, MPCConfig
     from koopman_mpc_portfolio_rebalancing_amd.backtest import run_backtest_lockstep
     N, L, H = 100, 256, 10
@@ -477,8 +479,16 @@ def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     S = int(out["return"].shape[1])
-    return {"workload": f"{P} lock-stepped backtest paths x {S} steps, C3 model ({N} assets, latent {L}, H={H}), "
-                        "run_backtest_lockstep defaults", "path_steps_per_s": P * S / el, "ms_per_step": el / S * 1e3,
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loop = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False)
+    torch.cuda.synchronize()
+    el_loop = time.perf_counter() - t0
+    return {"workload": f"{P} backtest paths x {S} steps, C3 model ({N} assets, latent {L}, H={H}), "
+                        "run_backtest_lockstep defaults (path-persistent kernel)",
+            "path_steps_per_s": P * S / el, "ms_per_step": el / S * 1e3,
+            "lockstep_loop_path_steps_per_s": P * S / el_loop,
+            "bit_identical_to_loop": bool(torch.equal(out["portfolio_value"], loop["portfolio_value"])),
             "r04_path_steps_per_s": 30.5e3}
 
 
