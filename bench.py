@@ -479,6 +479,7 @@ def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     S = int(out["return"].shape[1])
+    run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False)   # (warm-up: its streams, first calls)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loop = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False)

@@ -9,6 +9,9 @@ import bench
 from koopman_mpc_portfolio_rebalancing_amd import (BacktestConfig, DeviceKoopman, KoopmanModelSpec, KoopmanMPCStrategy,
                                                    MPCConfig)
 from koopman_mpc_portfolio_rebalancing_amd.backtest import run_backtest_lockstep
+from koopman_mpc_portfolio_rebalancing_amd import _lib
+if os.environ.get("KMPC_DEV_LIB"):   # a variant library built by csrc/Makefile (tvar / var)
+    _lib._lib = _lib.load(os.path.join(os.path.dirname(_lib.LIB_PATH), os.environ["KMPC_DEV_LIB"]))
 
 dev = torch.device("cuda", 0)
 N, L, H = 100, 256, 10
