@@ -12,7 +12,47 @@
 #include "kmpc_bt_step.h"
 
 namespace kmpc {
+namespace {
+// The mixed pair in one launch: each workgroup runs its window's float32 phase and then its float64
+// finish (the same two window bodies as the PH = 1 / PH = 2 kernels, kmpc_ipm_body.inc), so the
+// warm record is read back by the CU that wrote it and there is one launch tail instead of two.
+template <int HM, int MAXT, bool EXACT, int FL, int CS, bool QL, int GL>
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(1))) ipm_mixed_kernel(SolveArgs args) {
+    constexpr int NWM = MAXT / WAVE;
+    __shared__ union U {
+        Shared<HM, NWM, float> f;
+        Shared<HM, NWM, double> d;
+    } shu;
+    const int b = blockIdx.x;
+    if (b >= args.B) return;
+    [&]() __attribute__((always_inline)) {
+        constexpr int PH = 1;
+        using Real = float;
+        auto& sh = shu.f;
+#include "kmpc_ipm_body.inc"
+    }();
+    __syncthreads();   // the window's record written by every lane; the LDS structure reused
+    [&]() __attribute__((always_inline)) {
+        constexpr int PH = 2;
+        using Real = double;
+        auto& sh = shu.d;
+#include "kmpc_ipm_body.inc"
+    }();
+}
+}  // namespace
+
+#ifndef KMPC_MIXED_FUSED   // 1: the float32 phase and the float64 finish in one launch (ipm_mixed_kernel)
+#define KMPC_MIXED_FUSED 1
+#endif
+
 int launch_ipm_c3(const SolveArgs& a, hipStream_t stream) {
+    if (a.warm && KMPC_MIXED_FUSED) {
+        const size_t lds = cold_bytes<10, 128, QL_CS, true, 64, 7, double>();
+        hipLaunchKernelGGL((ipm_mixed_kernel<10, 128, true, 7, QL_CS, true, 64>), dim3(a.B), dim3(128), lds, stream, a);
+        int rc = hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+        if (rc == KMPC_OK) rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 3>(a, 128, stream);
+        return rc;
+    }
     if (a.warm) {   // mixed precision: the float32 phase, then the float64 finish from its iterates
         int rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 1>(a, 128, stream);
         if (rc == KMPC_OK) rc = launch_one<10, 128, true, 7, QL_CS, true, 64, 2>(a, 128, stream);
