@@ -13,17 +13,21 @@ import sqlite3
 import sys
 
 
-KERNEL = "%ipm_kernel<10, 128, true, 7%"   # the C3 launch (the bench also runs other ipm_kernel instances)
+# the C3 solve call's launches: ipm_mixed_kernel (float32 phase + float64 finish) and the retry
+# ipm_kernel<..., 3> (the bench also runs other instances: the float64-only PH = 0 of the lock-step loop)
+KERNEL = "%ipm_%kernel<10, 128, true, 7%"
+EXCLUDE = "%, 64, 0>%"
 
 
 def mean(db, counter):
     """Per solve call: the mean per dispatch of each kernel instance matching KERNEL, summed over
-    the instances (the mixed-precision call dispatches the float32 phase, the float64 finish and
-    the retry pass once each)."""
+    the instances (the mixed-precision call dispatches the fused float32 phase + float64 finish
+    and the retry pass once each)."""
     con = sqlite3.connect(db)
     try:
         rows = con.execute("select kernel_name, avg(value) from counters_collection where kernel_name like ? "
-                           "and counter_name = ? group by kernel_name", (KERNEL, counter)).fetchall()
+                           "and kernel_name not like ? and counter_name = ? group by kernel_name",
+                           (KERNEL, EXCLUDE, counter)).fetchall()
     finally:
         con.close()
     vals = [float(v) for _, v in rows if v is not None]
@@ -33,8 +37,8 @@ def mean(db, counter):
 def kernel_name(db):
     con = sqlite3.connect(db)
     try:
-        r = con.execute("select distinct kernel_name from counters_collection where kernel_name like ?",
-                        (KERNEL,)).fetchall()
+        r = con.execute("select distinct kernel_name from counters_collection where kernel_name like ? "
+                        "and kernel_name not like ?", (KERNEL, EXCLUDE)).fetchall()
     finally:
         con.close()
     return " + ".join(x[0] for x in r) if r else None
