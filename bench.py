@@ -690,7 +690,7 @@ def main():
         pmc = json.load(open(PMC_JSON)) if os.path.exists(PMC_JSON) and (N, H) == (100, 10) else None
         traffic = (pmc["fetch_bytes_per_window"] + pmc["write_bytes_per_window"]) * B if pmc else None
         roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": "kmpc_solve (ipm_kernel, register IPM)",
+                "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": "kmpc_solve (ipm_mixed_kernel: float32 phase + float64 finish, then the retry ipm_kernel; register IPM)",
                 "launch_ms": solve_ms, "algorithmic_bytes_per_window": solve_bytes // B,
                 "windows_per_launch": B}
         # what actually bounds the solve: f64 issue / latency. Executed f64 FLOPs per window from the
