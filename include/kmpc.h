@@ -245,9 +245,10 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
  *   weights [P,N] f64, value [P] f64, hist [P,S,4]: as kmpc_backtest_step, updated in place.
  *   target [P,N] f64, status [P] int, obj [P] f64: scratch (on return: the last step's W0, status,
  *             objective).
- * KMPC_ERR_UNSUPPORTED unless kmpc_solve would solve a batch of P such windows with the float64
- * register kernel of the BASELINE C3 shape (H = 10, 64 < N < 104, no short, cost and cap, float64
- * for this batch size); the caller then runs the lock-step loop. */
+ * KMPC_ERR_UNSUPPORTED unless kmpc_solve would solve a batch of P such windows with a float64
+ * one-window-per-workgroup register kernel of the constant case (no short, cost and cap; H = 10 or
+ * 5; 32 < N <= 256 — the BASELINE C3 shape among them — and not the mixed pair, i.e. float64 for
+ * this batch size); the caller then runs the lock-step loop. */
 int kmpc_backtest_run(const kmpc_backtest_desc* desc, const kmpc_solve_desc* sdesc, int step0, int n_steps,
                       const float* yhat, const float* realized, int n_real, double* weights, double* value,
                       double* hist, double* target, int* status, double* obj, void* stream);

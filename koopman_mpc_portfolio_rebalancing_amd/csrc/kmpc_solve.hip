@@ -357,9 +357,10 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     return KMPC_ERR_UNSUPPORTED;   // H > 10: the large-window kernel
 }
 
-// kmpc_backtest_run: the path-persistent kernel exists for the shape whose per-step batch of P
-// windows kmpc_solve sends to the float64 C3 kernel (ipm_kernel<10, 128, true, 7, QL_CS, true>):
-// H = 10, 64 < N < QL_CS, no short, cost and cap, float64 for this batch (not mixed_case)
+// kmpc_backtest_run: a path-persistent kernel exists for the shapes whose per-step batch of P
+// windows kmpc_solve sends to a float64 constant-case register kernel (case 7: no short, cost and
+// cap; H = 10 or 5, N <= 256, one window per workgroup — not the packed N <= 32 kernels, not the
+// mixed pair): the persistent kernel runs that kernel's window body, so the steps match it
 int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd, int step0, int n_steps,
                         const float* yhat, const float* realized, int n_real, double* weights, double* value,
                         double* hist, double* target, int* status, double* obj, hipStream_t stream) {
@@ -367,16 +368,31 @@ int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd,
     d.B = bd->P;
     SolveArgs a = make_args(&d);
     const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
-    if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || !fl7 || a.H != 10 || a.N <= 64 ||
-        a.N >= QL_CS)
+    const bool packed = a.path != KMPC_PATH_REGISTER_UNPACKED && a.N <= 32 && a.H <= 10;
+    if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || packed || !fl7 || a.N > 256 ||
+        (a.H != 10 && a.H != 5))
         return KMPC_ERR_UNSUPPORTED;
     if (a.path != KMPC_PATH_AUTO && a.path != KMPC_PATH_REGISTER && a.path != KMPC_PATH_REGISTER_UNPACKED)
         return KMPC_ERR_UNSUPPORTED;
+    const int nt = 64 * ((a.N + 63) / 64);
+#ifdef KMPC_DEV_ONLY_H10   // (dev builds link the C3 unit only)
+    if (!(a.H == 10 && nt == 128 && a.N < QL_CS)) return KMPC_ERR_UNSUPPORTED;
+#endif
     if (bd->P == 0 || n_steps == 0) return KMPC_OK;
     a.wout = target; a.status = status; a.obj = obj; a.iters = nullptr; a.trace = nullptr;
     a.yhat = yhat; a.wp = weights;
-    return launch_bt_run_c3(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value,
-                            hist, stream);
+    if (a.H == 10 && nt == 128 && a.N < QL_CS)
+        return launch_bt_run_c3(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value,
+                                hist, stream);
+#ifndef KMPC_DEV_ONLY_H10
+    if (a.H == 5)
+        return launch_bt_run_case<5>(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights,
+                                     value, hist, stream);
+    return launch_bt_run_case<10>(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value,
+                                  hist, stream);
+#else
+    return KMPC_ERR_UNSUPPORTED;
+#endif
 }
 
 }  // namespace kmpc

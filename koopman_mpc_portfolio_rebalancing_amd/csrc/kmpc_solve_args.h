@@ -51,6 +51,10 @@ int launch_ipm_c3(const SolveArgs& a, hipStream_t stream);
 // [P, N] W0 scratch, a.status / a.obj [P] scratch; n_steps steps from history row step0
 int launch_bt_run_c3(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
                      int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream);
+// ... and of the constant-case shapes H = HM (kmpc_solve_hbt*.hip); KMPC_ERR_UNSUPPORTED elsewhere
+template <int HM>
+int launch_bt_run_case(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
+                       int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream);
 // packed small-window kernels, 64 / GL windows per wave (kmpc_solve_p*.hip); KMPC_ERR_UNSUPPORTED
 // outside N <= 32, 3 H <= 32
 template <int HM>

@@ -197,17 +197,19 @@ def test_lockstep_path_groups_on_streams_equal_one_group(P, groups):
         assert torch.equal(v, grp["metrics"][k]), k
 
 
-@pytest.mark.parametrize("P,T,chunk", [(64, 22, None), (61, 19, 128)])
-def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, monkeypatch):
+@pytest.mark.parametrize("P,T,chunk,N,H", [(64, 22, None, 100, 10), (61, 19, 128, 100, 10), (24, 14, None, 100, 5),
+                                             (20, 15, None, 50, 10), (16, 14, None, 150, 10), (12, 12, None, 200, 5)])
+def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, N, H, monkeypatch):
     """run_backtest_lockstep(persistent=True): every step of every path in kmpc_backtest_run launches
     (one workgroup per path: the step's solve, then its bookkeeping, back to back) against the
     lock-step loop (one kmpc_solve over the P windows + one kmpc_backtest_step per step): the same
     window solve and bookkeeping code, so histories, weights and metrics are bit-identical. P = 61
-    with 2 steps per rollout chunk: several launches, each resuming the paths' state."""
+    with 2 steps per rollout chunk: several launches, each resuming the paths' state. The other
+    shapes: the constant-case kernels' persistent forms (64-, 128- and 256-thread windows, H = 5)."""
     import bench
     from koopman_mpc_portfolio_rebalancing_amd import backtest as bt
     dev = torch.device("cuda")
-    N, L, H = 100, 256, 10
+    L = 256
     obs_n = N * 20
     spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
     strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
@@ -229,11 +231,11 @@ def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, monkeypatch):
 
 
 def test_persistent_backtest_unsupported_shape():
-    """persistent=True on a shape without a persistent kernel (H = 5) raises; the default falls back
-    to the lock-step loop."""
+    """persistent=True on a shape without a persistent kernel (N = 20: the packed kernels) raises;
+    the default falls back to the lock-step loop."""
     import bench
     dev = torch.device("cuda")
-    N, L, H, P, T = 100, 256, 5, 8, 9
+    N, L, H, P, T = 20, 256, 5, 8, 9
     obs_n = N * 20
     spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
     strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")

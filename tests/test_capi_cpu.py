@@ -79,8 +79,13 @@ def test_argument_errors_need_no_gpu():
     assert run(0, 0, None, None, 1) == -1                     # more realized rows than steps
     sd.precision = 2                                          # MIXED: the per-step batch runs the pair
     assert run(0, 0, None, None, 0) == -2
-    sd.precision, sd.H = 0, 5                                 # another horizon: no persistent kernel
+    sd.precision, sd.H = 0, 5                                 # H = 5 constant-case kernels: supported
+    assert run(0, 0, None, None, 0) == 0
+    sd.H = 7                                                  # another horizon: no persistent kernel
     assert run(0, 0, None, None, 0) == -2
+    sd.H, sd.N, btr.N = 5, 20, 20                             # N <= 32: the packed kernels, no persistent form
+    assert run(0, 0, None, None, 0) == -2
+    sd.N, btr.N = 100, 100
     sd.H, sd.cost_coeff = 10, -1.0                            # the solve's own checks apply
     assert run(0, 0, None, None, 0) == -1
     bt.P = 0
