@@ -74,6 +74,9 @@ __host__ __device__ inline int slots_for(int B, int N) {
     return B < cap ? B : cap;
 }
 constexpr double LR_FLOOR = 1e-14;
+#ifndef KMPC_BIG_PF2S   // the Gram generator and Newton back-substitution / Zq sweeps: loads two periods ahead (1) or one (0)
+#define KMPC_BIG_PF2S 1
+#endif
 #ifndef KMPC_BIG_WPE   // waves per SIMD of the >= 512-thread kernels: 2 workgroups per CU
 #define KMPC_BIG_WPE 4
 #endif
@@ -547,18 +550,24 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
             v.bp = W.ht() ? (double)W.fat(A_BP, t) : 0.0;
             return v;
         };
-        Gv gnx{};
+        Gv gnx{}, gnx2{};
         double pi = 1.0;
         if (W.act) {
             pi = W.at(A_X, 0);
             gnx = ldG(H - 1);
+            if (KMPC_BIG_PF2S && H > 1) gnx2 = ldG(H - 2);
         }
         double dqn = 0.0, lrn = 0.0, gn = 0.0, bn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double vvn = 0.0;
             if (W.act) {
                 const Gv c = gnx;
-                if (t > 0) gnx = ldG(t - 1);
+                if (KMPC_BIG_PF2S) {
+                    gnx = gnx2;
+                    if (t > 1) gnx2 = ldG(t - 2);
+                } else if (t > 0) {
+                    gnx = ldG(t - 1);
+                }
                 const double idd = c.idd, lr = c.lr;
                 const double dq = idd + lrn * lrn * dqn;
                 if (t + 1 < H) pi *= rcp(fmax(lrn, LR_FLOOR));
@@ -971,14 +980,22 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             v.lr = W.fat(A_LR, t);
             return v;
         };
-        Bv bn{};
-        if (W.act) bn = ldB(H - 1);
+        Bv bn{}, bn2{};
+        if (W.act) {
+            bn = ldB(H - 1);
+            if (KMPC_BIG_PF2S && H > 1) bn2 = ldB(H - 2);
+        }
         double xn = 0.0, lrn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double x = 0.0, va = 0.0, vv1 = 0.0, ep = 0.0;
             if (W.act) {
                 const Bv c = bn;
-                if (t > 0) bn = ldB(t - 1);
+                if (KMPC_BIG_PF2S) {
+                    bn = bn2;
+                    if (t > 1) bn2 = ldB(t - 2);
+                } else if (t > 0) {
+                    bn = ldB(t - 1);
+                }
                 x = c.y * c.idd + lrn * xn;
                 W.at(A_X, t) = x;
                 ep = ht ? sh.sr[t] * c.bp : 0.0;
@@ -1022,12 +1039,18 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 v.lr = W.fat(A_LR, t);
                 return v;
             };
-            Fv fn = ldF(0);
+            Fv fn = ldF(0), fn2{};
+            if (KMPC_BIG_PF2S && H > 1) fn2 = ldF(1);
             double y = 0.0;
             double epc = W.epsa(0);
             for (int t = 0; t < H; ++t) {
                 const Fv c = fn;
-                if (t + 1 < H) fn = ldF(t + 1);
+                if (KMPC_BIG_PF2S) {
+                    fn = fn2;
+                    if (t + 2 < H) fn2 = ldF(t + 2);
+                } else if (t + 1 < H) {
+                    fn = ldF(t + 1);
+                }
                 const double epn = (t + 1 < H) ? sh.sr[t + 1] * c.bpn : 0.0;
                 const double zq = W.alpha(t, c.m) * sh.q[3 * t + 1] + sh.q[3 * t + 2] + epc * sh.q[3 * t] -
                                   ((t + 1 < H) ? epn * sh.q[3 * t + 3] : 0.0);
@@ -1052,14 +1075,22 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             v.ds1 = (!first && hs && t + 1 < H) ? (double)W.at(A_DS, t + 1) : 0.0;
             return v;
         };
-        Cv cn{};
-        if (W.act) cn = ldC(H - 1);
+        Cv cn{}, cn2{};
+        if (W.act) {
+            cn = ldC(H - 1);
+            if (KMPC_BIG_PF2S && H > 1) cn2 = ldC(H - 2);
+        }
         double tn = 0.0, lrn = 0.0, dwn = 0.0, bpn = 0.0, Pn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double pxn = 0.0, px0 = 0.0;
             if (W.act) {
                 const Cv c = cn;
-                if (t > 0) cn = ldC(t - 1);
+                if (KMPC_BIG_PF2S) {
+                    cn = cn2;
+                    if (t > 1) cn2 = ldC(t - 2);
+                } else if (t > 0) {
+                    cn = ldC(t - 1);
+                }
                 const double tq = c.y * c.idd + lrn * tn;
                 tn = tq;
                 lrn = c.lr;
