@@ -74,8 +74,14 @@ __host__ __device__ inline int slots_for(int B, int N) {
     return B < cap ? B : cap;
 }
 constexpr double LR_FLOOR = 1e-14;
-#ifndef KMPC_BIG_PF2S   // the Gram generator and Newton back-substitution / Zq sweeps: loads two periods ahead (1) or one (0)
+// the Gram generator and Newton back-substitution / Zq sweeps: loads two periods ahead (1) or one
+// (0) — C5 64.7 -> 61.5 ms, N = 500 / H = 10 57.7 -> 55.7, N = 300 / H = 15 55.7 -> 53.6 (r05,
+// tools/ab_c5.sh, tools/ab_big.sh; same iterates)
+#ifndef KMPC_BIG_PF2S
 #define KMPC_BIG_PF2S 1
+#endif
+#ifndef KMPC_BIG_PF3S   // ... three periods ahead (dev A/B: C5 61.8 -> 64.9 ms, every shape slower; r05)
+#define KMPC_BIG_PF3S 0
 #endif
 #ifndef KMPC_BIG_WPE   // waves per SIMD of the >= 512-thread kernels: 2 workgroups per CU
 #define KMPC_BIG_WPE 4
@@ -550,19 +556,24 @@ __device__ __forceinline__ void ph_gram(Win<HM, FL>& W) {
             v.bp = W.ht() ? (double)W.fat(A_BP, t) : 0.0;
             return v;
         };
-        Gv gnx{}, gnx2{};
+        Gv gnx{}, gnx2{}, gnx3{};
         double pi = 1.0;
         if (W.act) {
             pi = W.at(A_X, 0);
             gnx = ldG(H - 1);
             if (KMPC_BIG_PF2S && H > 1) gnx2 = ldG(H - 2);
+            if (KMPC_BIG_PF3S && H > 2) gnx3 = ldG(H - 3);
         }
         double dqn = 0.0, lrn = 0.0, gn = 0.0, bn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double vvn = 0.0;
             if (W.act) {
                 const Gv c = gnx;
-                if (KMPC_BIG_PF2S) {
+                if (KMPC_BIG_PF3S) {
+                    gnx = gnx2;
+                    gnx2 = gnx3;
+                    if (t > 2) gnx3 = ldG(t - 3);
+                } else if (KMPC_BIG_PF2S) {
                     gnx = gnx2;
                     if (t > 1) gnx2 = ldG(t - 2);
                 } else if (t > 0) {
@@ -980,17 +991,22 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             v.lr = W.fat(A_LR, t);
             return v;
         };
-        Bv bn{}, bn2{};
+        Bv bn{}, bn2{}, bn3{};
         if (W.act) {
             bn = ldB(H - 1);
             if (KMPC_BIG_PF2S && H > 1) bn2 = ldB(H - 2);
+            if (KMPC_BIG_PF3S && H > 2) bn3 = ldB(H - 3);
         }
         double xn = 0.0, lrn = 0.0, epn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double x = 0.0, va = 0.0, vv1 = 0.0, ep = 0.0;
             if (W.act) {
                 const Bv c = bn;
-                if (KMPC_BIG_PF2S) {
+                if (KMPC_BIG_PF3S) {
+                    bn = bn2;
+                    bn2 = bn3;
+                    if (t > 2) bn3 = ldB(t - 3);
+                } else if (KMPC_BIG_PF2S) {
                     bn = bn2;
                     if (t > 1) bn2 = ldB(t - 2);
                 } else if (t > 0) {
@@ -1039,13 +1055,18 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
                 v.lr = W.fat(A_LR, t);
                 return v;
             };
-            Fv fn = ldF(0), fn2{};
+            Fv fn = ldF(0), fn2{}, fn3{};
             if (KMPC_BIG_PF2S && H > 1) fn2 = ldF(1);
+            if (KMPC_BIG_PF3S && H > 2) fn3 = ldF(2);
             double y = 0.0;
             double epc = W.epsa(0);
             for (int t = 0; t < H; ++t) {
                 const Fv c = fn;
-                if (KMPC_BIG_PF2S) {
+                if (KMPC_BIG_PF3S) {
+                    fn = fn2;
+                    fn2 = fn3;
+                    if (t + 3 < H) fn3 = ldF(t + 3);
+                } else if (KMPC_BIG_PF2S) {
                     fn = fn2;
                     if (t + 2 < H) fn2 = ldF(t + 2);
                 } else if (t + 1 < H) {
@@ -1075,17 +1096,22 @@ __device__ __forceinline__ void ph_lsolve(Win<HM, FL>& W, bool first, bool corr 
             v.ds1 = (!first && hs && t + 1 < H) ? (double)W.at(A_DS, t + 1) : 0.0;
             return v;
         };
-        Cv cn{}, cn2{};
+        Cv cn{}, cn2{}, cn3{};
         if (W.act) {
             cn = ldC(H - 1);
             if (KMPC_BIG_PF2S && H > 1) cn2 = ldC(H - 2);
+            if (KMPC_BIG_PF3S && H > 2) cn3 = ldC(H - 3);
         }
         double tn = 0.0, lrn = 0.0, dwn = 0.0, bpn = 0.0, Pn = 0.0;
         for (int t = H - 1; t >= 0; --t) {
             double pxn = 0.0, px0 = 0.0;
             if (W.act) {
                 const Cv c = cn;
-                if (KMPC_BIG_PF2S) {
+                if (KMPC_BIG_PF3S) {
+                    cn = cn2;
+                    cn2 = cn3;
+                    if (t > 2) cn3 = ldC(t - 3);
+                } else if (KMPC_BIG_PF2S) {
                     cn = cn2;
                     if (t > 1) cn2 = ldC(t - 2);
                 } else if (t > 0) {
