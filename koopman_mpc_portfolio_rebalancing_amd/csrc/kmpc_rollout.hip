@@ -996,6 +996,29 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps_x3_kernel(LatentArgs a,
     }
 }
 
+// Latent powers (round 5): for a linear latent step (z_t = z_{t-1} K, identity norm) and a one-layer
+// decoder, y_t = z_t D_N^T + b = z_0 (D_N (K^T)^t)^T + b, so the whole H-step loop is ONE GEMM of
+// z_0 against W = [W_1; ...; W_H], W_t = D_N (K^T)^t = W_{t-1} K^T ([H N, L], built by H small
+// GEMMs per call): L H N multiply-adds per window instead of H (L^2 + L N) — 3.6x fewer at C3
+// (L = 256, N = 100, H = 10). The same fp32 arithmetic (the GEMM form of the call), with the
+// rounding of the K products on the weights instead of the activations (checked against float64:
+// tests/test_rollout_gpu.py). From KMPC_LATPOW_MINB windows (the H small GEMMs are ~10 us).
+#ifndef KMPC_LATPOW
+#define KMPC_LATPOW 1
+#endif
+#ifndef KMPC_LATPOW_MINB
+#define KMPC_LATPOW_MINB 8192
+#endif
+__global__ void tile_epilogue_kernel(int H, int N, const float* bias, const float* mean, const float* stdv,
+                                     float* tb, float* tm, float* ts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= H * N) return;
+    const int n = i % N;
+    tb[i] = bias ? bias[n] : 0.0f;
+    tm[i] = mean[n];
+    ts[i] = stdv[n];
+}
+
 // the fused H-step kernel: fp32, one decoder layer, L % 32 == 0 and <= 512 (2 x 32 rows of z in
 // LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
 // descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
@@ -1142,6 +1165,7 @@ size_t rollout_workspace_bytes(const kmpc_rollout_desc* d) {
     const size_t part = B * (size_t)wmax < SPLITK_ELEMS ? B * (size_t)wmax : SPLITK_ELEMS;
     bytes += align256(sizeof(float) * SPLITK_BUF * part);          // split-K partials (small batches)
     bytes += align256((size_t)6 * d->L * (d->L + 32 * (size_t)((d->N + 31) / 32)));   // K^T, D bf16 planes
+    bytes += align256(sizeof(float) * (size_t)d->H * d->N * (d->L + 3));   // latent powers W_t, tiled epilogue
     return bytes;
 }
 
@@ -1207,14 +1231,18 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         p += align256(sizeof(float) * SPLITK_BUF * pe);
     }
     __bf16* planes = (__bf16*)p;   // K^T and decoder-row bf16 planes (latent_steps_x3_kernel)
+    p += align256((size_t)6 * L * (L + 32 * (size_t)((N + 31) / 32)));
+    float* Wpow = (float*)p;      // latent powers [H N, L], then the tiled bias / mean / std [3][H N]
     int rc;
+    const bool latpow = KMPC_LATPOW && latent_fusable(d) && Bn >= KMPC_LATPOW_MINB &&
+                        !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL);
     // Small batches (the fused 16-row latent loop below KMPC_LAT16_MAXB windows) read K in place and
     // skip the transpose launch (configs[1]: 0.194 -> 0.190 ms per step); at 65,536 windows the
     // in-place read costs the latent loop more than the launch, so K^T stays (A/B).
     const bool lat16 = latent_fusable(d) && (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES);
     const bool kdir = lat16 && Bn < KMPC_LAT16_MAXB;
     dim3 tg((L + 31) / 32, (L + 31) / 32);
-    if (!kdir) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
+    if (!kdir && !latpow) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
     if (d->model_kind == KMPC_MODEL_LISTA)
         hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->lista_S, St, L, L);
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
@@ -1222,7 +1250,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     // ---- encode ----
     int znparts = 0;   // > 0: z0 left as split-K partials for the fused latent loop to sum
     const bool zfuse = KMPC_Z0_FUSE && d->model_kind == KMPC_MODEL_GENERIC && latent_fusable(d) &&
-                       d->norm_fn != KMPC_NORM_BALL;
+                       d->norm_fn != KMPC_NORM_BALL && !latpow;
     if (d->model_kind == KMPC_MODEL_GENERIC) {
         rc = run_mlp(d->encoder, Bn, obs, obs_ld, z0, L, L, EPI_NONE, nullptr, nullptr, ping, pong, wmax, bf, s, part,
                      zfuse ? &znparts : nullptr);
@@ -1255,6 +1283,24 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (znparts > 0 && !latent_fusable(d)) return KMPC_ERR_INVALID;   // (zfuse implies fusable)
 
     // ---- H x (step_latent, decode[:N], destandardize) ----
+    if (latpow) {
+        const int HN = H * N;
+        float* tb = Wpow + (size_t)HN * L;
+        float* tm = tb + HN;
+        float* ts = tm + HN;
+        for (int t = 0; t < H; ++t) {   // W_1 = D_N K^T, W_t = W_{t-1} K^T (C = A B^T with B = K)
+            GemmArgs g = linear(N, L, L, t ? Wpow + (size_t)(t - 1) * N * L : d->decoder.weight[0], L, d->kmat,
+                                nullptr, Wpow + (size_t)t * N * L, L);
+            g.bf16 = bf;
+            if ((rc = gemm(g, s, part))) return rc;
+        }
+        hipLaunchKernelGGL(tile_epilogue_kernel, dim3((HN + 255) / 256), dim3(256), 0, s, H, N, d->decoder.bias[0],
+                           d->mean, d->std, tb, tm, ts);
+        GemmArgs g = linear(Bn, HN, L, z0, L, Wpow, tb, yhat, HN);   // yhat [B, H, N] = [B, H N]
+        g.epi = EPI_DESTD; g.mean = tm; g.stdv = ts; g.bf16 = bf;
+        if ((rc = gemm(g, s, part))) return rc;
+        return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+    }
     if (latent_fusable(d)) {
         LatentArgs la;
         la.B = Bn; la.L = L; la.N = N; la.H = H; la.z0 = z0; la.Kt = Kt; la.K = d->kmat; la.D = d->decoder.weight[0];
