@@ -998,17 +998,49 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps_x3_kernel(LatentArgs a,
 
 // Latent powers (round 5): for a linear latent step (z_t = z_{t-1} K, identity norm) and a one-layer
 // decoder, y_t = z_t D_N^T + b = z_0 (D_N (K^T)^t)^T + b, so the whole H-step loop is ONE GEMM of
-// z_0 against W = [W_1; ...; W_H], W_t = D_N (K^T)^t = W_{t-1} K^T ([H N, L], built by H small
-// GEMMs per call): L H N multiply-adds per window instead of H (L^2 + L N) — 3.6x fewer at C3
-// (L = 256, N = 100, H = 10). The same fp32 arithmetic (the GEMM form of the call), with the
-// rounding of the K products on the weights instead of the activations (checked against float64:
-// tests/test_rollout_gpu.py). From KMPC_LATPOW_MINB windows (the H small GEMMs are ~10 us).
+// z_0 against W = [W_1; ...; W_H], W_t = D_N (K^T)^t = W_{t-1} K^T ([H N, L], latent_powers_kernel
+// per call, float64 chains rounded once per W_t): L H N multiply-adds per window instead of
+// H (L^2 + L N) — 3.6x fewer at C3 (L = 256, N = 100, H = 10). The same fp32 GEMM arithmetic,
+// with the K products taken on the weights instead of the activations (checked against float64:
+// tests/test_rollout_gpu.py). From KMPC_LATPOW_MINB windows.
 #ifndef KMPC_LATPOW
 #define KMPC_LATPOW 1
 #endif
 #ifndef KMPC_LATPOW_MINB
 #define KMPC_LATPOW_MINB 8192
 #endif
+// W_t rows: one workgroup per decoder row i (rows are independent: W_t[i] = W_{t-1}[i] K^T), one
+// thread per column j, the row chain carried in float64 in LDS and each W_t rounded once to fp32;
+// Kt = K^T read coalesced (thread j reads Kt[k][j]). ~10 us where H GEMM launches took ~160 us.
+__global__ void latent_powers_kernel(const float* __restrict__ D, const float* __restrict__ Kt, int L, int N, int H,
+                                     float* __restrict__ W) {
+    extern __shared__ double prow[];   // [L]
+    const int i = blockIdx.x, j = threadIdx.x;
+    if (j < L) prow[j] = (double)D[(size_t)i * L + j];
+    __syncthreads();
+    for (int t = 0; t < H; ++t) {
+        double acc = 0.0;
+        if (j < L) {
+            // eight independent partial sums, sixteen loads in flight (L % 32 == 0: latent_fusable)
+            double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            for (int k0 = 0; k0 < L; k0 += 16) {
+                float kv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) kv[u] = Kt[(size_t)(k0 + u) * L + j];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) a[u & 7] = fma(prow[k0 + u], (double)kv[u], a[u & 7]);
+            }
+            acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        }
+        __syncthreads();
+        if (j < L) {
+            prow[j] = acc;
+            W[((size_t)t * N + i) * L + j] = (float)acc;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void tile_epilogue_kernel(int H, int N, const float* bias, const float* mean, const float* stdv,
                                      float* tb, float* tm, float* ts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1242,7 +1274,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     const bool lat16 = latent_fusable(d) && (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES);
     const bool kdir = lat16 && Bn < KMPC_LAT16_MAXB;
     dim3 tg((L + 31) / 32, (L + 31) / 32);
-    if (!kdir && !latpow) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
+    if (!kdir) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
     if (d->model_kind == KMPC_MODEL_LISTA)
         hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->lista_S, St, L, L);
     if (hipGetLastError() != hipSuccess) return KMPC_ERR_LAUNCH;
@@ -1288,12 +1320,9 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
         float* tb = Wpow + (size_t)HN * L;
         float* tm = tb + HN;
         float* ts = tm + HN;
-        for (int t = 0; t < H; ++t) {   // W_1 = D_N K^T, W_t = W_{t-1} K^T (C = A B^T with B = K)
-            GemmArgs g = linear(N, L, L, t ? Wpow + (size_t)(t - 1) * N * L : d->decoder.weight[0], L, d->kmat,
-                                nullptr, Wpow + (size_t)t * N * L, L);
-            g.bf16 = bf;
-            if ((rc = gemm(g, s, part))) return rc;
-        }
+        // W_1 = D_N K^T, W_t = W_{t-1} K^T (float64 chains per row, fp32 W_t)
+        hipLaunchKernelGGL(latent_powers_kernel, dim3(N), dim3(64 * ((L + 63) / 64)), sizeof(double) * L, s,
+                           d->decoder.weight[0], Kt, L, N, H, Wpow);
         hipLaunchKernelGGL(tile_epilogue_kernel, dim3((HN + 255) / 256), dim3(256), 0, s, H, N, d->decoder.bias[0],
                            d->mean, d->std, tb, tm, ts);
         GemmArgs g = linear(Bn, HN, L, z0, L, Wpow, tb, yhat, HN);   // yhat [B, H, N] = [B, H N]
