@@ -1006,7 +1006,7 @@ __global__ void __launch_bounds__(64 * NWV) latent_steps_x3_kernel(LatentArgs a,
 #ifndef KMPC_LATPOW
 #define KMPC_LATPOW 1
 #endif
-#ifndef KMPC_LATPOW_MINB
+#ifndef KMPC_LATPOW_MINB   // (at configs[1]'s 4,096 windows the fused 16-row loop is faster: 0.152 vs 0.159 ms per step)
 #define KMPC_LATPOW_MINB 8192
 #endif
 // W_t rows: one workgroup per decoder row i (rows are independent: W_t[i] = W_{t-1}[i] K^T), one
@@ -1272,7 +1272,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     // skip the transpose launch (configs[1]: 0.194 -> 0.190 ms per step); at 65,536 windows the
     // in-place read costs the latent loop more than the launch, so K^T stays (A/B).
     const bool lat16 = latent_fusable(d) && (Bn < KMPC_LAT16_MAXB || L <= 16 * KMPC_LAT16_WAVES);
-    const bool kdir = lat16 && Bn < KMPC_LAT16_MAXB;
+    const bool kdir = lat16 && Bn < KMPC_LAT16_MAXB && !latpow;   // (the powers kernel reads K^T)
     dim3 tg((L + 31) / 32, (L + 31) / 32);
     if (!kdir) hipLaunchKernelGGL(transpose_kernel, tg, dim3(256), 0, s, d->kmat, Kt, L, L);
     if (d->model_kind == KMPC_MODEL_LISTA)
