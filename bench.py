@@ -82,6 +82,22 @@ def solve_flop_model(N: int, H: int) -> dict:
     return {"per_iteration": sum(phases.values()), "phases": phases}
 
 
+LATPOW_MINB = 8192   # KMPC_LATPOW_MINB (kmpc_rollout.hip): the latent-powers GEMM from this many windows
+
+
+def best_f64_peak():
+    """The best f64 FMA rate tools/dev/f64_peak measured on MI355X in any round's profiles/*_f64_peak.txt
+    (independent v_fma_f64 chains on every CU; the 78.6 TF spec figure is not reached by it)."""
+    import glob
+    best, src = 0.0, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_f64_peak.txt"))):
+        import re
+        for v in re.findall(r"f64 fma: .*?([\d.]+) TFLOP/s", open(f).read()):
+            if float(v) * 1e12 > best:
+                best, src = float(v) * 1e12, os.path.relpath(f, ROOT)
+    return best, (f"measured: tools/dev/f64_peak, the best run in profiles/ ({src})" if src else None)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -97,6 +113,16 @@ def parse():
     p.add_argument("--hidden", type=int, default=1024)
     p.add_argument("--cpu-seconds", type=float, default=20.0,
                    help="approximate CPU-baseline budget (0 disables the cpu_baseline leg)")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend for N > 1 (nccl = RCCL over xGMI, the default; gloo moves "
+                        "the W0 gather and the timing collectives through host copies)")
+    p.add_argument("--share-device", action="store_true",
+                   help="every rank uses cuda:0 (a readiness check of the sharded path on a one-GPU box, "
+                        "with --backend gloo: not a scaling figure)")
+    p.add_argument("--headline-only", action="store_true",
+                   help="skip the secondary configurations and the CPU baselines")
+    p.add_argument("--dump-w0", default="",
+                   help="rank 0 saves the (gathered) W0 of the last timed step to this .npy file")
     return p.parse_args()
 
 
@@ -158,12 +184,13 @@ def window_inputs(lo: int, hi: int, N: int, obs: int, seed: int, device):
     return torch.cat(xs).contiguous(), torch.cat(ws).contiguous()
 
 
-def timed_loop(step, steps: int, warmup: int, world: int, device, info: dict = None):
+def timed_loop(step, steps: int, warmup: int, world: int, device, info: dict = None, comm_device=None):
     """The bench contract's timing: `warmup` untimed steps, then exactly `steps` steps bracketed by a
     barrier + device synchronize on both sides; the elapsed time is the MAX over ranks (all_reduce).
     step(k) runs one step (k = None for warmup) and returns its output; returns (elapsed, last).
     The warmup steps include the step's collective, so communicator setup is not timed.
-    info (optional) receives this rank's own elapsed time as "local_elapsed_s"."""
+    info (optional) receives this rank's own elapsed time as "local_elapsed_s". comm_device: where
+    the timing collective's tensor lives (default `device`; the CPU under gloo)."""
     import torch.distributed as dist
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
     out = None
@@ -184,7 +211,7 @@ def timed_loop(step, steps: int, warmup: int, world: int, device, info: dict = N
     if info is not None:
         info["local_elapsed_s"] = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_device or device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, out
@@ -625,12 +652,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     check_world(world, args.gpus)
     import torch.distributed as dist
+    gpu = 0 if args.share_device else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(gpu)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
         check_world(dist.get_world_size(), args.gpus)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
     torch.cuda.set_device(dev)
+    # collectives: on the device under RCCL, through host copies under gloo
+    comm = dev if args.backend == "nccl" else torch.device("cpu")
 
     from koopman_mpc_portfolio_rebalancing_amd import (DeviceKoopman, KoopmanModelSpec, MPCConfig,
                                                        solve_mpc_log_utility_batched)
@@ -654,13 +687,18 @@ def main():
     # one stream, one workspace), what KoopmanMPCStrategy.rebalance_batch runs
     def step(k):
         W0, st, val, its = model.window(x, wp, mean_d, std_d, N, cfg, with_iters=True)
-        if world > 1:
-            gather_rows(W0, G, world, rank, dst=0)    # the one RCCL collective
-        return W0, st, val, its
+        Wg = W0
+        if world > 1:   # the one RCCL collective
+            Wg = gather_rows(W0 if comm.type == "cuda" else W0.cpu(), G, world, rank, dst=0)
+        return W0, st, val, its, Wg
 
     tinfo = {}
-    elapsed, (W0, st, val, its) = timed_loop(step, args.steps, args.warmup, world, dev, tinfo)
-    prov = rank_provenance(B, tinfo["local_elapsed_s"], dev) if world > 1 else None
+    elapsed, (W0, st, val, its, Wg) = timed_loop(step, args.steps, args.warmup, world, dev, tinfo, comm)
+    prov = rank_provenance(B, tinfo["local_elapsed_s"], comm) if world > 1 else None
+    if prov is not None:
+        prov["share_device"] = bool(args.share_device)
+    if args.dump_w0 and rank == 0:
+        np.save(args.dump_w0, Wg.cpu().numpy())
 
     # kernel split, after the timed region: the same step as two C-ABI calls (kmpc_rollout, then
     # kmpc_solve), each bracketed by HIP events on the launch stream — the solve's launch time is
@@ -716,7 +754,7 @@ def main():
         if pmc and "f64_flops_per_window" in pmc:
             lanes = pmc.get("active_lane_fraction", N / (64 * -(-N // 64)))
             useful = pmc["f64_flops_per_window"] * lanes * B / (solve_ms * 1e-3)
-            peak = pmc.get("f64_peak_flops", F64_VALU_PEAK)
+            peak = best_f64_peak()[0] or pmc.get("f64_peak_flops", F64_VALU_PEAK)
             if "f32_flops_per_window" in pmc:
                 util["executed_f32_flops_per_window"] = pmc["f32_flops_per_window"]
             util.update({"executed_f64_flops_per_window": pmc["f64_flops_per_window"],
@@ -725,23 +763,33 @@ def main():
                          "frac": useful / peak, "counts_from": os.path.relpath(PMC_JSON, ROOT)})
         util.update({"algorithmic_achieved": alg * B / (solve_ms * 1e-3) / 1e12, "peak": peak / 1e12,
                      "algorithmic_frac": alg * B / (solve_ms * 1e-3) / peak,
-                     "peak_source": pmc.get("f64_peak_source", "spec") if pmc else "spec"})
-        roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L
-                                + H * (L * L + L * N))
+                     "peak_source": best_f64_peak()[1] if best_f64_peak()[0] else "spec"})
+        # rollout FLOPs the timed path EXECUTES: the encoder, then the latent loop as the library
+        # runs it at this batch size — from 8,192 windows (KMPC_LATPOW_MINB, identity norm) one GEMM
+        # of z_0 against the latent powers [H N, L] (L H N multiply-adds per window) plus the
+        # per-call powers chain (H N L^2, latent_powers_kernel); below it H (L^2 + L N) per window
+        latpow = B >= LATPOW_MINB
+        lat_flops = 2.0 * B * H * N * L + 2.0 * H * N * L * L if latpow else 2.0 * B * H * (L * L + L * N)
+        roll_flops = 2.0 * B * (obs * args.hidden + args.hidden * args.hidden + args.hidden * L) + lat_flops
         c4 = world > 1
         line = {
             "metric": METRIC, "value": value, "unit": "windows/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong" if c4 else "weak", "vs_baseline": None,
-            "dtype": "f32 rollout / f64 solve",
+            "dtype": "f32 rollout (fp32 GEMMs as three exact bf16 planes); mixed f32->f64 IPM solve "
+                     "(float32 phase to mu 5e-5, float64 finish: stopping rule, status and W in float64)",
             "data": "synthetic (seeded N(0,1) standardized embeddings, Dirichlet w_prev, random-init finance_sparse weights)",
             "config": {"workload": (f"C4 (BASELINE configs[3]): {G} windows/step over {world} GPUs" if c4 else
                                     f"C3 (BASELINE configs[2]): {G} windows/GPU") +
                                    f", {N} assets, latent {L}, H={H}, obs {obs}, GenericKM enc "
                                    f"[{args.hidden},{args.hidden}], L1-turnover MPC c=1e-3 tau=0.2 no-short",
                        "windows_per_gpu": B, "global_windows_per_step": G,
-                       "parallelism": (f"windows sharded over {world} GPUs (contiguous blocks of one global "
-                                       f"stream), RCCL gather of W0 to rank 0" if c4 else "1 GPU, no collective")}
+                       "parallelism": ((f"windows sharded over {world} ranks sharing cuda:0 (readiness check, not "
+                                        f"a scaling figure), {args.backend} gather of W0 to rank 0")
+                                       if args.share_device and c4 else
+                                       f"windows sharded over {world} GPUs (contiguous blocks of one global "
+                                       f"stream), {'RCCL' if args.backend == 'nccl' else 'gloo'} gather of W0 to rank 0"
+                                       if c4 else "1 GPU, no collective")}
                       | ({"dist": prov} if prov else {}),
             "roofline": roof,
             "compute_utilization": util,
@@ -760,17 +808,20 @@ def main():
                         "rollout_tflops": roll_flops / (roll_ms * 1e-3) / 1e12,
                         "rollout_frac_of_f32_mfma_peak": roll_flops / (roll_ms * 1e-3) / FP32_MFMA_PEAK,
                         "rollout_bf16_mfma_executed_frac": 6 * roll_flops / (roll_ms * 1e-3) / BF16_MFMA_PEAK,
-                        "rollout_gemm_form": "fp32 as three exact bf16 planes on v_mfma_f32_32x32x16_bf16"},
+                        "rollout_gemm_form": "fp32 as three exact bf16 planes on v_mfma_f32_32x32x16_bf16",
+                        "rollout_flops_counted": "executed: encoder + " + (
+                            "latent powers GEMM (2 L H N per window) + the per-call powers chain (2 H N L^2)"
+                            if latpow else "sequential latent loop (2 H (L^2 + L N) per window)")},
             "solver": {"optimal_or_inaccurate": n_opt, "windows": B,
                        "mean_ipm_iterations": float(its.float().mean().item())},
         }
         line["rollout_parity"] = rollout_parity(model, sd, x, mean_d, std_d, H, N)
-        if world == 1:
+        if world == 1 and not args.headline_only:
             line["secondary"] = secondary_c2(dev, args.steps, args.warmup)
             line["secondary_c1"] = secondary_c1(dev, args.steps, args.warmup)
             line["secondary_c5"] = secondary_c5(dev, min(args.steps, 3), min(args.warmup, 1))
             line["secondary_lockstep"] = secondary_lockstep(dev)
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and args.cpu_seconds > 0 and not args.headline_only:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base
             line["cpu_baseline_serial"] = cpu_baseline_serial(sd, mean, std, x, wp, H, N, cfg,

@@ -158,6 +158,10 @@ typedef struct kmpc_mlp {
     const float* bias[KMPC_MAX_LAYERS];
 } kmpc_mlp;
 
+#define KMPC_LATENT_AUTO       0   /* kmpc_rollout_desc.latent_unfused */
+#define KMPC_LATENT_UNFUSED    1
+#define KMPC_LATENT_SEQUENTIAL 2
+
 typedef struct kmpc_rollout_desc {
     int B;            /* windows                                                  */
     int N;            /* assets (first N outputs of the decoder, data_finance.py:729) */
@@ -188,8 +192,14 @@ typedef struct kmpc_rollout_desc {
     int dtype;                /* KMPC_DTYPE_F32 (0, the reference's fp32 arithmetic), KMPC_DTYPE_BF16
                                  (1: GEMM operands rounded to bf16 on MFMA, fp32 accumulation and
                                  epilogues; BASELINE configs[4]) or KMPC_DTYPE_F32_F32MFMA (2)   */
-    int latent_unfused;       /* 0: the H-step loop runs as one fused launch where the model allows
-                                 it; 1: one GEMM launch per step (same arithmetic; A/B and tests)  */
+    int latent_unfused;       /* the H-step latent loop (KMPC_LATENT_*, same fp32 arithmetic up to
+                                 summation order; A/B and tests):
+                                 0 AUTO: the library's choice — from KMPC_LATPOW_MINB (8,192) windows
+                                   with a linear latent step (norm 'id', LISTA) one GEMM of z_0 against
+                                   the latent powers D_N (K^T)^t, else one fused launch;
+                                 1 UNFUSED: one GEMM launch per step;
+                                 2 SEQUENTIAL: the fused step-by-step loop at every batch size
+                                   (ABI 0.6.0; the three-plane latent_steps_x3_kernel at L = 256) */
 } kmpc_rollout_desc;
 
 int kmpc_rollout(const kmpc_rollout_desc* desc,
@@ -316,7 +326,7 @@ const char* kmpc_strerror(int code);
    callers built against an older ABI must rebuild. 0.4.0 added enum values only
    (KMPC_PRECISION_MIXED, KMPC_DTYPE_F32_F32MFMA; AUTO precision now float64 below KMPC_MIXED_MIN_B
    windows; KMPC_DTYPE_F32's GEMMs on three bf16 planes), no layout change. 0.5.0 added a function
-   (kmpc_backtest_run), no layout change. */
+   (kmpc_backtest_run), no layout change. 0.6.0 added enum values only (KMPC_LATENT_SEQUENTIAL). */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

@@ -24,6 +24,7 @@ MODEL_GENERIC, MODEL_LISTA = 0, 1
 ACT = {"relu": 0, "tanh": 1, "gelu": 2}
 NORM = {"id": 0, "ball": 1}
 DTYPE = {"fp32": 0, "bf16": 1, "fp32_f32mfma": 2}
+LATENT_FORM = {"auto": 0, "unfused": 1, "sequential": 2}   # kmpc_rollout_desc.latent_unfused (KMPC_LATENT_*)
 
 STATUS_NAMES = {0: "optimal", 1: "optimal_inaccurate", 2: "infeasible", 3: "unbounded",
                 4: "solver_error"}
@@ -43,8 +44,9 @@ MIXED_MIN_B = 2048   # KMPC_MIXED_MIN_B: AUTO runs the mixed pair from this many
 # ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
 # kmpc_rollout_desc.latent_unfused, 0.3.0 kmpc_solve_desc.precision and .mu_handoff, so an older
 # library would read them past its structs' end; 0.4.0 added enum values only (KMPC_PRECISION_MIXED,
-# KMPC_DTYPE_F32_F32MFMA), no layout change; 0.5.0 added kmpc_backtest_run
-ABI_VERSION = "0.5.0"
+# KMPC_DTYPE_F32_F32MFMA), no layout change; 0.5.0 added kmpc_backtest_run;
+# 0.6.0 enum values only (KMPC_LATENT_SEQUENTIAL)
+ABI_VERSION = "0.6.0"
 
 
 class KmpcError(RuntimeError):

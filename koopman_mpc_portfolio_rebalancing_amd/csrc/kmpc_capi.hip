@@ -26,7 +26,7 @@ int check_solve(const kmpc_solve_desc* d) {
 
 extern "C" {
 
-const char* kmpc_version(void) { return "kmpc 0.5.0 (gfx950)"; }
+const char* kmpc_version(void) { return "kmpc 0.6.0 (gfx950)"; }
 
 const char* kmpc_strerror(int code) {
     switch (code) {

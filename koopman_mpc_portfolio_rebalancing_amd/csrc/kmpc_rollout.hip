@@ -1053,9 +1053,10 @@ __global__ void tile_epilogue_kernel(int H, int N, const float* bias, const floa
 
 // the fused H-step kernel: fp32, one decoder layer, L % 32 == 0 and <= 512 (2 x 32 rows of z in
 // LDS: 132 KB at L = 512), decoder rows read with 16-byte loads (16-byte aligned base); the
-// descriptor's latent_unfused forces the per-step launches (A/B and the GPU test that compares both)
+// descriptor's latent_unfused = KMPC_LATENT_UNFUSED forces the per-step launches, KMPC_LATENT_SEQUENTIAL
+// the fused step-by-step loop even where the latent powers would run (A/B and the GPU tests)
 static bool latent_fusable(const kmpc_rollout_desc* d) {
-    return !d->latent_unfused && d->dtype != KMPC_DTYPE_BF16 && d->decoder.n_layers == 1 && d->L % 32 == 0 &&
+    return d->latent_unfused != KMPC_LATENT_UNFUSED && d->dtype != KMPC_DTYPE_BF16 && d->decoder.n_layers == 1 && d->L % 32 == 0 &&
            d->L <= 512 && ((uintptr_t)d->decoder.weight[0] & 15) == 0 &&
            !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn != KMPC_NORM_ID && d->norm_fn != KMPC_NORM_BALL);
 }
@@ -1239,6 +1240,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     if (d->obs_ld < 0 || (d->obs_ld > 0 && d->obs_ld < d->N)) return KMPC_ERR_INVALID;
     if (d->dtype != KMPC_DTYPE_F32 && d->dtype != KMPC_DTYPE_BF16 && d->dtype != KMPC_DTYPE_F32_F32MFMA)
         return KMPC_ERR_INVALID;
+    if (d->latent_unfused < KMPC_LATENT_AUTO || d->latent_unfused > KMPC_LATENT_SEQUENTIAL) return KMPC_ERR_INVALID;
     // GemmArgs::bf16: 2 = three bf16 planes (fp32 arithmetic), 1 = bf16 operands, 0 = f32-input MFMA
     const int bf = d->dtype == KMPC_DTYPE_F32 ? KMPC_F32_GEMM : d->dtype == KMPC_DTYPE_BF16 ? 1 : 0;
     if (d->B == 0) return KMPC_OK;
@@ -1266,7 +1268,7 @@ int rollout_launch(const kmpc_rollout_desc* d, const float* obs, float* yhat, vo
     p += align256((size_t)6 * L * (L + 32 * (size_t)((N + 31) / 32)));
     float* Wpow = (float*)p;      // latent powers [H N, L], then the tiled bias / mean / std [3][H N]
     int rc;
-    const bool latpow = KMPC_LATPOW && latent_fusable(d) && Bn >= KMPC_LATPOW_MINB &&
+    const bool latpow = KMPC_LATPOW && d->latent_unfused == KMPC_LATENT_AUTO && latent_fusable(d) && Bn >= KMPC_LATPOW_MINB &&
                         !(d->model_kind == KMPC_MODEL_GENERIC && d->norm_fn == KMPC_NORM_BALL);
     // Small batches (the fused 16-row latent loop below KMPC_LAT16_MAXB windows) read K in place and
     // skip the transpose launch (configs[1]: 0.194 -> 0.190 ms per step); at 65,536 windows the

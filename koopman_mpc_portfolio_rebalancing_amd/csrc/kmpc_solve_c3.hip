@@ -7,6 +7,17 @@
 #include "kmpc_solve_kernel.h"
 #include "kmpc_bt_run.h"
 
+#ifndef KMPC_REG_HANDOFF_ON   // ipm_mixed_kernel's handoff: 2 LDS, 1 registers, 0 the warm record in HBM
+#define KMPC_REG_HANDOFF_ON 2
+#endif
+
+namespace kmpc {
+// the handoff's LDS slot of this lane (as the cold arrays: lanes past CS - 1 share its slot, an
+// inactive asset whose values are never read)
+template <int CS>
+__device__ __forceinline__ int hand_lane() { const int t = (int)threadIdx.x; return t < CS ? t : CS - 1; }
+}
+
 namespace kmpc {
 namespace {
 // The mixed pair in one launch: each workgroup runs its window's float32 phase and then its float64
@@ -21,19 +32,34 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(1))) 
     } shu;
     const int b = blockIdx.x;
     if (b >= args.B) return;
+#if KMPC_REG_HANDOFF_ON
+    // the float32 phase's iterate handed to the float64 finish on chip, not
+    // through the 20 KB warm record in HBM: each lane's w, s, l1..l3 for its asset and the period
+    // owners' z4, l4, nu — in the finish's cold-array LDS (2, the default: free during the float32
+    // phase) or in registers (1: live across the phase boundary; 12 more spilled VGPRs in the finish)
+    static_assert(KMPC_REG_HANDOFF_ON != 2 || (5 * HM * CS + 3 * HM) * 4 <= cold_bytes<HM, MAXT, CS, QL, GL, FL, double>(),
+                  "the handoff fits the float64 cold arrays' LDS");
+#if KMPC_REG_HANDOFF_ON == 1
+    float hand_w[HM], hand_s[HM], hand_l1[HM], hand_l2[HM], hand_l3[HM];
+    float hand_z4 = 1.0f, hand_l4 = 0.0f, hand_nu = 0.0f;
+#endif
+    bool hand_flag = false;
+#define KMPC_REG_HANDOFF
+#endif
     [&]() __attribute__((always_inline)) {
         constexpr int PH = 1;
         using Real = float;
         auto& sh = shu.f;
 #include "kmpc_ipm_body.inc"
     }();
-    __syncthreads();   // the window's record written by every lane; the LDS structure reused
+    __syncthreads();   // the window's header written; the LDS structure reused
     [&]() __attribute__((always_inline)) {
         constexpr int PH = 2;
         using Real = double;
         auto& sh = shu.d;
 #include "kmpc_ipm_body.inc"
     }();
+#undef KMPC_REG_HANDOFF
 }
 }  // namespace
 

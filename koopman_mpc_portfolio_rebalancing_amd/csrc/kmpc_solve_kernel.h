@@ -553,6 +553,12 @@ constexpr size_t cold_bytes() { return cold_in_lds<HM, MAXT, CS, QL, GL, FL, Rea
 
 // ---- shared state -------------------------------------------------------------------------------
 
+// lsolve's never-taken branch that steered the register allocation (r04: +2.8% on the float64 C3
+// solve); 0 drops it (dev A/B of VERDICT r05 item 8)
+#ifndef KMPC_LSOLVE_STEER
+#define KMPC_LSOLVE_STEER 1
+#endif
+
 template <int HM, int NWM, class Real = double>
 struct Shared {
     static constexpr int KM = 3 * HM;
@@ -1034,7 +1040,7 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM, typename TH:
 #pragma unroll
             for (int t = 0; t < HM; ++t)
                 px[t] = t < H ? (-T.c - sh.l4[t] - (T.ht ? sh.lb5[t] * sh.iz4[t] : Real(0.0))) * sh.sp[t] : Real(0.0);
-        } else if (T.N < 0) {
+        } else if (KMPC_LSOLVE_STEER && T.N < 0) {
             // Never taken (N >= 1: the C ABI rejects the rest). Kept because this branch's presence
             // changes the register allocation of the whole kernel: 46 -> 41 spilled VGPRs and +2.8%
             // on the C3 solve, measured r04 (tools/ab_run.sh, two repeats; the compiler drops a

@@ -59,6 +59,14 @@ class KoopmanModelSpec:
     lista_thresh: float = 0.0
 
     @property
+    def fuse_latent(self) -> bool:
+        return self.latent_form != "unfused"
+
+    @fuse_latent.setter
+    def fuse_latent(self, v: bool) -> None:
+        self.latent_form = "auto" if v else "unfused"
+
+    @property
     def latent(self) -> int:
         return int(self.kmat.shape[0])
 
@@ -111,13 +119,19 @@ class DeviceKoopman:
     """A KoopmanModelSpec resident on one device, evaluated through kmpc_rollout / kmpc_window."""
 
     def __init__(self, spec: KoopmanModelSpec, device: Optional[torch.device] = None, dtype: str = "fp32",
-                 fuse_latent: bool = True):
+                 fuse_latent: bool = True, latent_form: str = "auto"):
         """dtype: 'fp32' (the reference's arithmetic, default: GEMMs on the bf16 MFMA with every fp32
         operand split exactly into three bf16 planes — an fp32 GEMM in accuracy), 'fp32_f32mfma' (the
         same arithmetic on the f32-input MFMA) or 'bf16' (GEMM operands rounded to bf16 on the bf16
-        MFMA, fp32 accumulation — BASELINE configs[4]). fuse_latent=False runs the
-        H-step loop as one GEMM launch per step (kmpc_rollout_desc.latent_unfused; A/B and tests)."""
-        self.fuse_latent = bool(fuse_latent)
+        MFMA, fp32 accumulation — BASELINE configs[4]). latent_form (kmpc_rollout_desc.latent_unfused)
+        picks how the H-step latent loop runs: 'auto' (the library's choice: the latent-powers GEMM
+        from 8,192 windows where the latent step is linear, else one fused launch), 'sequential' (the
+        fused step-by-step loop at every batch size: latent_steps_x3_kernel at L = 256 on three bf16
+        planes, the fp32 loops otherwise) or 'unfused' (one GEMM launch per step); fuse_latent=False
+        is 'unfused'. All three are the same fp32 arithmetic up to summation order (A/B and tests)."""
+        if latent_form not in _lib.LATENT_FORM:
+            raise ValueError(f"latent_form must be one of {sorted(_lib.LATENT_FORM)}")
+        self.latent_form = latent_form if fuse_latent else "unfused"
         if dtype not in _lib.DTYPE:
             raise ValueError(f"dtype must be one of {sorted(_lib.DTYPE)}")
         self.dtype = dtype
@@ -139,6 +153,14 @@ class DeviceKoopman:
         self.S = up(spec.lista_S)
         if len(self.enc) > _lib.KMPC_MAX_LAYERS or len(self.dec) > _lib.KMPC_MAX_LAYERS:
             raise _lib.KmpcError("too many layers for kmpc_mlp")
+
+    @property
+    def fuse_latent(self) -> bool:
+        return self.latent_form != "unfused"
+
+    @fuse_latent.setter
+    def fuse_latent(self, v: bool) -> None:
+        self.latent_form = "auto" if v else "unfused"
 
     @property
     def latent(self) -> int:
@@ -170,7 +192,7 @@ class DeviceKoopman:
         d.encoder = self._mlp(enc if enc is not None else self.enc, s.enc_act, s.enc_last_relu)
         d.obs_ld = int(obs_ld)
         d.dtype = _lib.DTYPE[self.dtype]
-        d.latent_unfused = int(not self.fuse_latent)
+        d.latent_unfused = _lib.LATENT_FORM[self.latent_form]
         d.lista_S = self.S.data_ptr() if self.S is not None else None
         d.lista_loops = int(s.lista_loops)
         d.lista_thresh = float(s.lista_thresh)

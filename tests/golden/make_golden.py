@@ -11,6 +11,8 @@ What it records (all float data, no code):
   mpc_*.npz       MPC problems (w_prev, yhat, numpy's float32 R = np.exp(yhat), config) with the
                   long-double oracle optimum
                   (oracle/kmpc_oracle.c), plus SLSQP / dense-IPM cross-checks where small enough.
+  headline_*.npz  the bench's models (weights regenerated from their seed by the test) run through
+                  the reference's GenericKM and rebalance op order on 64 windows: obs, stats, yhat.
   backtest_*.npz  reference run_backtest + calculate_metrics (backtest.py:133-249) on a synthetic
                   FinanceEnv built with the reference's data_finance functions; the MPC solve inside
                   KoopmanMPCStrategy is routed to the oracle (cvxpy is not installed here), and every
@@ -182,6 +184,54 @@ def make_rollout_goldens():
         print("rollout", name, yhat.shape, float(np.abs(yhat).max()))
 
 
+HEADLINE_CASES = [  # name, N, emb, latent, hidden, H, weight seed, obs seed (bench.py's models)
+    ("c3", 100, 20, 256, 1024, 10, 0, 0),    # BASELINE configs[2]: the bench's headline model
+    ("c2", 30, 20, 128, 1024, 5, 1, 100),    # configs[1] (bench.secondary_c2)
+    ("c1", 10, 20, 128, 1024, 5, 10, 10),    # configs[0] (bench.secondary_c1 / cpu_baseline_c1)
+]
+HEADLINE_WINDOWS = 64
+
+
+def state_checksums(sd):
+    """float64 sum and sum of squares per tensor: binds a golden to the weights the test regenerates."""
+    return {k: [float(v.double().sum()), float((v.double() ** 2).sum())] for k, v in sd.items()}
+
+
+def make_headline_goldens():
+    """The bench's own models (bench.make_state_dict, finance_sparse GenericKM layout) loaded into the
+    reference's GenericKM (model.py:701-797, strict load_state_dict), rolled out by the reference's
+    rebalance op order (backtest.py:99-121: encode, then H x step_latent / decode / extract /
+    destandardize, batch 1 per window) on 64 windows of the bench's input stream. Only the
+    observations, the de-standardisation stats, the yhat and weight checksums are stored: the test
+    regenerates the weights from the seed and tiles the 64 rows to the batch sizes whose kernels it
+    pins (the latent-powers GEMM path from 8,192 windows, the fused latent loops below)."""
+    import bench
+    for name, N, emb, L, hidden, H, wseed, xseed in HEADLINE_CASES:
+        obs_n = N * emb
+        cfg = ref_config.get_config("finance_sparse")
+        cfg.MODEL.TARGET_SIZE = L
+        cfg.MODEL.ENCODER.LAYERS = [hidden, hidden]
+        model = ref_model.make_model(cfg, obs_n)
+        sd = bench.make_state_dict(obs_n, L, hidden, seed=wseed)
+        model.load_state_dict(sd, strict=True)
+        model.eval()
+        # per-asset stats (not constants), through the reference's own FinanceEnv methods
+        mean = np.linspace(-8e-4, 1.2e-3, N)
+        std = np.linspace(0.01, 0.025, N)
+        env = types.SimpleNamespace(n_assets=N, stats=ref_data.FinanceStats(mean, std, [f"A{i}" for i in range(N)]))
+        env.extract_current_returns = types.MethodType(ref_data.FinanceEnv.extract_current_returns, env)
+        env.destandardize_returns = types.MethodType(ref_data.FinanceEnv.destandardize_returns, env)
+        x, _ = bench.window_inputs(0, HEADLINE_WINDOWS, N, obs_n, seed=xseed, device=torch.device("cpu"))
+        obs = x.numpy().astype(np.float32)
+        yhat = reference_yhat(model, env, obs, H)
+        meta = {"N": N, "emb": emb, "L": L, "hidden": hidden, "H": H, "weight_seed": wseed, "obs_seed": xseed,
+                "checksums": state_checksums(sd), "torch": torch.__version__,
+                "generator": "tests/golden/make_golden.py make_headline_goldens"}
+        np.savez_compressed(os.path.join(HERE, f"headline_{name}.npz"), obs=obs, yhat=yhat, mean=mean, std=std,
+                            meta=json.dumps(meta))
+        print("headline", name, yhat.shape, float(np.abs(yhat).max()))
+
+
 def make_mpc_goldens():
     rng = np.random.default_rng(2024)
     # reference test_mpc cases with their exact optima (tests/test_mpc.py:6-55 of the reference)
@@ -336,7 +386,9 @@ def make_embedding_goldens():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding", "dmd"]
+    which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding", "dmd", "headline"]
+    if "headline" in which:
+        make_headline_goldens()
     if "dmd" in which:
         make_dmd_goldens()
     if "embedding" in which:

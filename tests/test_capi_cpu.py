@@ -213,3 +213,6 @@ def test_python_constants_match_the_header():
     assert defs["KMPC_DTYPE_F32"] == _lib.DTYPE["fp32"]
     assert defs["KMPC_DTYPE_BF16"] == _lib.DTYPE["bf16"]
     assert defs["KMPC_DTYPE_F32_F32MFMA"] == _lib.DTYPE["fp32_f32mfma"]
+    assert defs["KMPC_LATENT_AUTO"] == _lib.LATENT_FORM["auto"]
+    assert defs["KMPC_LATENT_UNFUSED"] == _lib.LATENT_FORM["unfused"]
+    assert defs["KMPC_LATENT_SEQUENTIAL"] == _lib.LATENT_FORM["sequential"]

@@ -213,12 +213,17 @@ def test_bf16_lista_rollout_at_config5_shape():
 @pytest.mark.parametrize("norm,L,N,B,H", [("id", 64, 20, 1000, 4), ("ball", 64, 40, 333, 3),
                                           ("id", 128, 30, 4096, 5), ("ball", 256, 100, 70, 10),
                                           ("id", 512, 50, 300, 6),     # L = 512: 132 KB of LDS
-                                          ("ball", 64, 20, 8200, 3),   # >= 8192 windows: 32-row blocks
+                                          ("ball", 64, 20, 8200, 3),   # >= 8192, ball: the 16-row loop
+                                          ("ball", 256, 40, 8200, 3),  # >= 8192, ball, L = 256: 32-row loop
                                           ("id", 256, 100, 8200, 10), ("id", 256, 33, 8193, 2)])  # ragged
 def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
-    """The one-launch H-step loop (latent_steps_kernel: L % 32 == 0, single-layer decoder; 16 windows
-    per block below 8,192 windows, 32 from there) against the per-step GEMM launches
-    (kmpc_rollout_desc.latent_unfused) and the numpy restatement."""
+    """The fused H-step latent loops (L % 32 == 0, single-layer decoder) against the per-step GEMM
+    launches (KMPC_LATENT_UNFUSED) and the numpy restatement. Which kernel runs (kmpc_rollout.hip):
+    below 8,192 windows, or L <= 128, the 16-row loop (latent_steps16_kernel); from 8,192 windows with
+    the identity norm the library's default ('auto') is the latent-powers GEMM (latent_powers_kernel
+    + one three-plane GEMM with the de-standardising epilogue), and 'sequential' forces the
+    step-by-step loop there — latent_steps_x3_kernel at L = 256 — so both are checked; the ball norm
+    (nonlinear step) at L = 256 runs the 32-row fp32 loop (latent_steps_kernel)."""
     import bench
     obs, hidden = N * 4, 64
     sd = bench.make_state_dict(obs, L, hidden, seed=3)
@@ -228,7 +233,9 @@ def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
     mean = np.linspace(-1e-3, 1e-3, N).astype(np.float32)
     std = np.linspace(0.01, 0.02, N).astype(np.float32)
     yf = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
-    km.fuse_latent = False                     # kmpc_rollout_desc.latent_unfused: per-step launches
+    km.latent_form = "sequential"
+    ys = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
+    km.latent_form = "unfused"                 # KMPC_LATENT_UNFUSED: per-step launches
     yu = km.rollout(x.cuda(), mean, std, H, N).cpu().numpy()
     sdn = {k: v.numpy() for k, v in sd.items()}
     spec_np = {"kind": "generic", "enc_w": [sdn[f"encoder.network.{i}.weight"] for i in (0, 2, 4)],
@@ -236,7 +243,51 @@ def test_fused_latent_steps_match_unfused_and_numpy(norm, L, N, B, H):
                "dec_w": [sdn["decoder.network.0.weight"]], "dec_b": [None], "norm_fn": norm}
     ref = R.rollout(spec_np, x.numpy(), H, N, mean, std)
     assert_rel(yf - ref, np.abs(ref).max(), 1e-5, f"fused {norm} L{L} B{B}")
+    assert_rel(ys - ref, np.abs(ref).max(), 1e-5, f"sequential {norm} L{L} B{B}")
     assert_rel(yf - yu, np.abs(yu).max(), 1e-5, f"fused-vs-unfused {norm} L{L} B{B}")
+    if norm == "ball" or B < 8192:   # the same kernel either way: bit-identical
+        assert np.array_equal(yf, ys)
+
+
+HEADLINE = sorted(glob.glob(os.path.join(GOLD, "headline_*.npz")))
+
+
+def _headline(path):
+    """A headline golden (tests/golden/make_golden.py make_headline_goldens) and its model: the
+    bench's weights regenerated from their seed, checked against the golden's checksums."""
+    import bench
+    g = np.load(path)
+    m = json.loads(str(g["meta"]))
+    sd = bench.make_state_dict(m["N"] * m["emb"], m["L"], m["hidden"], seed=m["weight_seed"])
+    for k, v in sd.items():
+        s1, s2 = m["checksums"][k]
+        assert float(v.double().sum()) == pytest.approx(s1, rel=1e-12, abs=1e-12), k
+        assert float((v.double() ** 2).sum()) == pytest.approx(s2, rel=1e-12), k
+    return g, m, KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG)
+
+
+@pytest.mark.parametrize("form", ["auto", "sequential"])
+@pytest.mark.parametrize("path", HEADLINE, ids=[os.path.basename(p)[9:-4] for p in HEADLINE])
+def test_headline_rollout_matches_reference(path, form):
+    """The bench's own models (c3 = BASELINE configs[2]: obs 2000, encoder [1024, 1024], latent 256,
+    N = 100, H = 10; c2 = configs[1]; c1 = configs[0]) against yhat from the reference's GenericKM and
+    rebalance op order on 64 windows (reference model.py:701-797, backtest.py:99-121). The 64 rows are
+    tiled to 64, 4,096, 8,200 (ragged) and 65,536 windows, so every kernel that produced a bench
+    window is pinned at the 2e-6 bar of the reference goldens: the three-plane encoder GEMMs at all
+    tile shapes, and for the latent loop the 16-row kernel below 8,192 windows and, from 8,192,
+    the latent-powers GEMM ('auto', the bench's path) or the step-by-step loop ('sequential':
+    latent_steps_x3_kernel at L = 256). Every row of every tile is compared with its source row."""
+    g, m, spec = _headline(path)
+    N, H = m["N"], m["H"]
+    km = DeviceKoopman(spec, torch.device("cuda"), latent_form=form)
+    obs = torch.from_numpy(g["obs"]).cuda()
+    ref = g["yhat"]
+    scale = np.abs(ref).max()
+    for B in (64, 4096, 8200, 65536):
+        idx = torch.arange(B, device="cuda") % obs.shape[0]
+        y = km.rollout(obs[idx].contiguous(), g["mean"], g["std"], H, N).cpu().numpy()
+        d = y - ref[np.arange(B) % ref.shape[0]]
+        assert_rel(d, scale, 2e-6, f"{os.path.basename(path)} {form} B{B}")
 
 
 def test_small_batch_split_k_encoder_matches_numpy():
@@ -368,10 +419,11 @@ def test_fp32_gemm_forms_against_float64(B, N, L, H, obs):
 
 def test_three_plane_paths_lista_and_unaligned_rows():
     """The three-plane fp32 paths off the bench shapes, at >= 8,192 windows with L = 256 (the large
-    GEMM tiles and latent_steps_x3_kernel): (1) LISTAKM (linear We, 10 loops: the shrink-epilogue
-    GEMMs and the LISTA z0 into the plane latent loop); (2) GenericKM with obs = 99 (rows not a
-    multiple of 4 floats: the scalar operand fetch) and N = 33. Each against the numpy fp32
-    restatement and the f32-input MFMA form (1e-5 of the decoded scale, the fp32 rollout bars)."""
+    GEMM tiles; the latent loop as the library's default — the latent-powers GEMM — and as
+    'sequential', latent_steps_x3_kernel): (1) LISTAKM (linear We, 10 loops: the shrink-epilogue
+    GEMMs and the LISTA z0 into the latent loop); (2) GenericKM with obs = 99 (rows not a multiple of
+    4 floats: the scalar operand fetch) and N = 33. Each against the numpy fp32 restatement and the
+    f32-input MFMA form (1e-5 of the decoded scale, the fp32 rollout bars)."""
     import bench
     rng = np.random.default_rng(9)
     B, L, H = 8200, 256, 4
@@ -390,21 +442,25 @@ def test_three_plane_paths_lista_and_unaligned_rows():
                             lista_loops=10, lista_thresh=float(5e-3 / lip))
     obs = rng.standard_normal((B, obs_n)).astype(np.float32)
     mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
-    y = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
     y1 = DeviceKoopman(spec, torch.device("cuda"), dtype="fp32_f32mfma").rollout(
         torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
     ref = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
-    assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, "three-plane lista L256")
-    assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, "three-plane vs f32-input lista L256")
+    for form in ("auto", "sequential"):
+        y = DeviceKoopman(spec, torch.device("cuda"), latent_form=form).rollout(
+            torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+        assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, f"three-plane lista L256 {form}")
+        assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, f"three-plane vs f32-input lista L256 {form}")
     # (2) GenericKM, obs 99
     N, obs_n = 33, 99
     sd = bench.make_state_dict(obs_n, L, 512, seed=7)
     spec = KoopmanModelSpec.from_state_dict(sd, bench.MODEL_CFG)
     obs = rng.standard_normal((B, obs_n)).astype(np.float32)
     mean, std = np.full(N, 5e-4, np.float32), np.full(N, 0.015, np.float32)
-    y = DeviceKoopman(spec, torch.device("cuda")).rollout(torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
     y1 = DeviceKoopman(spec, torch.device("cuda"), dtype="fp32_f32mfma").rollout(
         torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
     ref = R.rollout(_oracle_spec(spec), obs, H, N, mean, std)
-    assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, "three-plane generic obs99")
-    assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, "three-plane vs f32-input generic obs99")
+    for form in ("auto", "sequential"):
+        y = DeviceKoopman(spec, torch.device("cuda"), latent_form=form).rollout(
+            torch.from_numpy(obs).cuda(), mean, std, H, N).cpu().numpy()
+        assert_rel(y - ref, np.abs(ref - mean).max(), 1e-5, f"three-plane generic obs99 {form}")
+        assert_rel(y - y1, np.abs(ref - mean).max(), 1e-5, f"three-plane vs f32-input generic obs99 {form}")
