@@ -481,18 +481,19 @@ def secondary_c1(dev, steps: int, warmup: int, B: int = 65536) -> dict:
             "optimal_or_inaccurate": int((st.cpu().numpy() <= 1).sum()), "windows": B}
 
 
-def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
+def secondary_lockstep(dev, P: int = 64, T: int = 130, N: int = 100, L: int = 256, H: int = 10,
+                       seed: int = 0) -> dict:
     """SURVEY §8(f) row 1 at a small path count: P backtest paths of the
-    headline model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2) over T test rows,
+    headline model (100 assets, latent 256, H = 10, c = 1e-3, tau = 0.2; or, with N = 10, L = 128,
+    H = 5, seed 10, the configs[0] model — VERDICT r05 item 7) over T test rows,
     run_backtest_lockstep with its defaults (forecasts rolled out up front, then every step of every
     path in one path-persistent launch, kmpc_backtest_run; bit-identical to the lock-step loop);
     path-steps/s = P x steps / wall time of the second of two identical runs. Beside it the
     lock-step loop (three path groups on streams) for comparison."""
     from koopman_mpc_portfolio_rebalancing_amd import BacktestConfig, KoopmanModelSpec, KoopmanMPCStrategy, MPCConfig
     from koopman_mpc_portfolio_rebalancing_amd.backtest import run_backtest_lockstep
-    N, L, H = 100, 256, 10
     obs = N * 20
-    spec = KoopmanModelSpec.from_state_dict(make_state_dict(obs, L, 1024, seed=0), MODEL_CFG)
+    spec = KoopmanModelSpec.from_state_dict(make_state_dict(obs, L, 1024, seed=seed), MODEL_CFG)
     strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device=str(dev))
     g = torch.Generator().manual_seed(0)
     x = torch.randn(P, T, obs, generator=g).to(dev)
@@ -512,12 +513,14 @@ def secondary_lockstep(dev, P: int = 64, T: int = 130) -> dict:
     loop = run_backtest_lockstep(strat, x, r, cfg, mean, std, persistent=False)
     torch.cuda.synchronize()
     el_loop = time.perf_counter() - t0
-    return {"workload": f"{P} backtest paths x {S} steps, C3 model ({N} assets, latent {L}, H={H}), "
-                        "run_backtest_lockstep defaults (path-persistent kernel)",
-            "path_steps_per_s": P * S / el, "ms_per_step": el / S * 1e3,
-            "lockstep_loop_path_steps_per_s": P * S / el_loop,
-            "bit_identical_to_loop": bool(torch.equal(out["portfolio_value"], loop["portfolio_value"])),
-            "r04_path_steps_per_s": 30.5e3}
+    res = {"workload": f"{P} backtest paths x {S} steps, {'C3' if N == 100 else 'configs[0]'} model ({N} assets, "
+                       f"latent {L}, H={H}), run_backtest_lockstep defaults (path-persistent kernel)",
+           "path_steps_per_s": P * S / el, "ms_per_step": el / S * 1e3,
+           "lockstep_loop_path_steps_per_s": P * S / el_loop, "speedup_vs_loop": el_loop / el,
+           "bit_identical_to_loop": bool(torch.equal(out["portfolio_value"], loop["portfolio_value"]))}
+    if N == 100:
+        res["r04_path_steps_per_s"] = 30.5e3
+    return res
 
 
 def make_lista_state_dict(obs: int, L: int, seed: int = 0) -> dict:
@@ -821,6 +824,7 @@ def main():
             line["secondary_c1"] = secondary_c1(dev, args.steps, args.warmup)
             line["secondary_c5"] = secondary_c5(dev, min(args.steps, 3), min(args.warmup, 1))
             line["secondary_lockstep"] = secondary_lockstep(dev)
+            line["secondary_lockstep_c1"] = secondary_lockstep(dev, N=10, L=128, H=5, seed=10)
         if world == 1 and args.cpu_seconds > 0 and not args.headline_only:
             base, parity = cpu_baseline(sd, mean, std, x, wp, W0, val, y, H, N, cfg, args.cpu_seconds)
             line["cpu_baseline"] = base

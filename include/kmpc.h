@@ -256,9 +256,11 @@ int kmpc_backtest_step(const kmpc_backtest_desc* desc, int step, const double* t
  *   target [P,N] f64, status [P] int, obj [P] f64: scratch (on return: the last step's W0, status,
  *             objective).
  * KMPC_ERR_UNSUPPORTED unless kmpc_solve would solve a batch of P such windows with a float64
- * one-window-per-workgroup register kernel of the constant case (no short, cost and cap; H = 10 or
- * 5; 32 < N <= 256 — the BASELINE C3 shape among them — and not the mixed pair, i.e. float64 for
- * this batch size); the caller then runs the lock-step loop. */
+ * register kernel of the constant case (no short, cost and cap) — one window per workgroup for
+ * H = 10 or 5 and 32 < N <= 256 (the BASELINE C3 shape among them), or (ABI 0.6.0) the packed
+ * kernels for N <= 32 and H = 2, 5 or 10 (BASELINE configs[0]'s 10 assets, H = 5: one path per
+ * lane group, 64 / GL paths per wave) — and not the mixed pair, i.e. float64 for this batch size;
+ * the caller then runs the lock-step loop. */
 int kmpc_backtest_run(const kmpc_backtest_desc* desc, const kmpc_solve_desc* sdesc, int step0, int n_steps,
                       const float* yhat, const float* realized, int n_real, double* weights, double* value,
                       double* hist, double* target, int* status, double* obj, void* stream);
@@ -326,7 +328,8 @@ const char* kmpc_strerror(int code);
    callers built against an older ABI must rebuild. 0.4.0 added enum values only
    (KMPC_PRECISION_MIXED, KMPC_DTYPE_F32_F32MFMA; AUTO precision now float64 below KMPC_MIXED_MIN_B
    windows; KMPC_DTYPE_F32's GEMMs on three bf16 planes), no layout change. 0.5.0 added a function
-   (kmpc_backtest_run), no layout change. 0.6.0 added enum values only (KMPC_LATENT_SEQUENTIAL). */
+   (kmpc_backtest_run), no layout change. 0.6.0 added enum values only (KMPC_LATENT_SEQUENTIAL) and
+   kmpc_backtest_run's packed shapes, no layout change. */
 const char* kmpc_version(void);
 
 #ifdef __cplusplus

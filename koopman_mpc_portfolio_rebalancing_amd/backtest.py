@@ -250,9 +250,10 @@ def run_backtest_lockstep(strategy: KoopmanMPCStrategy, obs, realized, config: B
         persistent: run every step of a path in one launch (kmpc_backtest_run: one workgroup per
             path, the step's solve then its bookkeeping, back to back) — no lock step at all, so a
             path never waits for another path's window. Default: with prerollout, without graph or
-            groups, wherever the C ABI has the kernel for the shape (the C3 shape in float64: the
-            kernel kmpc_solve would use for the per-step batch); bit-identical to the lock-step
-            loop. Falls back to the loop where unsupported.
+            groups, wherever the C ABI has the kernel for the shape (the float64 constant-case
+            kernels kmpc_solve would use for the per-step batch: the C3 shape, 32 < N <= 256 at
+            H = 5 / 10, and the packed N <= 32 shapes at H = 2 / 5 / 10 — one path per lane group);
+            bit-identical to the lock-step loop. Falls back to the loop where unsupported.
     Returns: dict of device tensors — portfolio_value / return / turnover / cost [P, S] (the
         reference DataFrame columns), weights [P, N] (after the last step), metrics {name: [P]}.
     """

@@ -19,18 +19,26 @@ struct BtRun {
     bt::StepArgs st;         // bookkeeping: st.k = the first step's history row; st.target = W0 scratch
 };
 
-// One workgroup per path (window index b = path). The per-step solve is the float64 kernel
-// ipm_kernel<HM, MAXT, EXACT, FL, CS, QL, 64, 0> (the one kmpc_solve picks for a batch of
-// P < KMPC_MIXED_MIN_B such windows), so every step's W0 matches the lock-step run's.
+// One workgroup per path (window index b = path), or for the packed kernels (GL < 64: N <= 32)
+// one GL-lane group per path, 64 / GL paths per one-wave workgroup. The per-step solve is the
+// float64 kernel ipm_kernel<HM, MAXT, EXACT, FL, CS, QL, GL, 0> (the one kmpc_solve picks for a batch
+// of P < KMPC_MIXED_MIN_B such windows), so every step's W0 matches the lock-step run's. The paths of
+// one packed wave step together (a path whose window has converged waits, masked, for its wave's
+// slowest), but never for the rest of the batch.
 template <int HM, int MAXT, bool EXACT, int FL, int CS, bool QL, int GL, int PH>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(HM <= KMPC_WPE2_HM ? 2 : 1)))
 bt_run_kernel(SolveArgs a0, BtRun r) {
-    static_assert(PH == 0 && GL == 64, "float64 whole-wave windows");
+    static_assert(PH == 0, "float64 windows");
+    static_assert(GL == 64 || MAXT == 64, "lane groups pack one-wave blocks");
     using Real = double;
     constexpr int NWM = MAXT / WAVE;
-    __shared__ Shared<HM, NWM, Real> shv[1];
+    constexpr int WPB = GL == 64 ? 1 : 64 / GL;   // paths per block
+    __shared__ Shared<HM, NWM, Real> shv[WPB];
     __shared__ double red[NWM];
-    auto& sh = shv[0];
+    auto& sh = shv[grp<GL>()];
+    if constexpr (GL < 64) {
+        if ((int)blockIdx.x * WPB + grp<GL>() >= a0.B) return;   // (whole groups of the last block)
+    }
     const size_t PHN = (size_t)a0.B * a0.H * a0.N, PN = (size_t)a0.B * a0.N;
     for (int k = 0; k < r.n_steps; ++k) {
         {
@@ -39,21 +47,24 @@ bt_run_kernel(SolveArgs a0, BtRun r) {
             // (laundering b and the argument fields every step — nothing derived from them hoisted
             // out of the loop — cut the scratch from 512 to 448 B per lane but ran slower: P = 64
             // 0.898 -> 0.913 ms per step, P = 1,024 1.92 -> 1.98 ms)
-            const int b = blockIdx.x;
+            const int b = blockIdx.x * WPB + grp<GL>();
 #include "kmpc_ipm_body.inc"
         }
         __syncthreads();   // W0 (st.target) of every lane, and the solve's LDS, done
         bt::StepArgs st = r.st;
         st.k = r.st.k + k;
         st.realized = k < r.n_real ? r.realized + k * PN : nullptr;
-        bt::bt_step_body(st, blockIdx.x, red);
+        if constexpr (GL == 64)
+            bt::bt_step_body(st, blockIdx.x, red);
+        else
+            bt::bt_step_group<GL>(st, blockIdx.x * WPB + grp<GL>(), gvt<GL>());
         __syncthreads();   // the drifted weights are the next solve's w_prev
     }
 }
 
 
 // the launch: a.B = paths, a.wout the [P, N] W0 scratch, a.status / a.obj [P] scratch
-template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false>
+template <int HM, int MAXT, bool EXACT, int FL, int CS = MAXT, bool QL = false, int GL = 64>
 int launch_bt_run_one(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
                       int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream) {
     BtRun r;
@@ -65,10 +76,30 @@ int launch_bt_run_one(const SolveArgs& a, int n_steps, int n_real, const float* 
     r.st.target = a.wout; r.st.realized = nullptr; r.st.w = weights; r.st.value = value; r.st.hist = hist;
     SolveArgs s = a;
     s.wp = weights;   // each step's w_prev: the path's current (drifted) weights
-    const size_t lds = cold_bytes<HM, MAXT, CS, QL, 64, FL, double>();
-    hipLaunchKernelGGL((bt_run_kernel<HM, MAXT, EXACT, FL, CS, QL, 64, 0>), dim3(a.B), dim3(64 * ((a.N + 63) / 64)),
-                       lds, stream, s, r);
+    const size_t lds = cold_bytes<HM, MAXT, CS, QL, GL, FL, double>();
+    constexpr int WPB = GL == 64 ? 1 : 64 / GL;
+    hipLaunchKernelGGL((bt_run_kernel<HM, MAXT, EXACT, FL, CS, QL, GL, 0>), dim3((a.B + WPB - 1) / WPB),
+                       dim3(GL == 64 ? 64 * ((a.N + 63) / 64) : 64), lds, stream, s, r);
     return hipGetLastError() == hipSuccess ? KMPC_OK : KMPC_ERR_LAUNCH;
+}
+
+// The packed shapes (launch_ipm_packed<HM>'s choice for case 7 with H = HM: N <= 32, 3 HM <= 32):
+// KMPC_ERR_UNSUPPORTED elsewhere (a ragged H runs the generic packed kernel: no persistent form).
+template <int HM>
+int launch_bt_run_packed(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
+                         int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream) {
+    const int fl = case_of(!a.allow_short, a.c > 0.0 || a.tau > 0.0, a.tau > 0.0);
+    if (a.H != HM || a.N > 32 || 3 * HM > 32 || fl != 7) return KMPC_ERR_UNSUPPORTED;
+#define KMPC_BT_ARGS a, n_steps, n_real, yhat, realized, step0, S, c, weights, value, hist, stream
+    if constexpr (3 * HM <= 16) {
+        if (a.N <= 16) {
+            if (a.N <= KMPC_PACK_NS - 1) return launch_bt_run_one<HM, 64, true, 7, 4 * KMPC_PACK_NS, false, 16>(KMPC_BT_ARGS);
+            return launch_bt_run_one<HM, 64, true, 7, 64, false, 16>(KMPC_BT_ARGS);
+        }
+    }
+    if constexpr (3 * HM <= 32) return launch_bt_run_one<HM, 64, true, 7, 64, false, 32>(KMPC_BT_ARGS);
+#undef KMPC_BT_ARGS
+    return KMPC_ERR_UNSUPPORTED;
 }
 
 // The constant-case shapes (launch_ipm_case<HM>'s choice for case 7: no short + cost + cap, H = HM,

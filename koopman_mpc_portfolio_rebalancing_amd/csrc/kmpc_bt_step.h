@@ -71,5 +71,51 @@ __device__ __forceinline__ void bt_step_body(const StepArgs& a, int p, double* r
     }
 }
 
+// The same step for a path on a GL-lane group of a packed wave (N <= GL, lane i owns asset i):
+// the lock-step kernel's sums restricted to the group. There (one 64-lane wave for N <= 64) the
+// butterfly levels at and above GL add exact zeros (lanes past N hold 0), and the levels below GL
+// are these, in the same order; its total then starts from 0.0 — so the results are bit-identical
+// to bt_step_body's (tests/test_backtest_gpu.py, persistent vs lock-step).
+template <int GL>
+__device__ __forceinline__ double group_sum_bt(double v) {
+#pragma unroll
+    for (int o = GL / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return 0.0 + v;
+}
+
+template <int GL>
+__device__ __forceinline__ void bt_step_group(const StepArgs& a, int p, int i) {
+    const double* tg = a.target + (size_t)p * a.N;
+    double* w = a.w + (size_t)p * a.N;
+    const bool on = i < a.N;
+    const double tgi = on ? tg[i] : 0.0;
+    const double wi = on ? w[i] : 0.0;
+    const double turnover = group_sum_bt<GL>(on ? 0.0 + fabs(tgi - wi) : 0.0);
+    double value = a.value[p];
+    const double cost = a.c * turnover * value;
+    value -= cost;
+    double port = 0.0;
+    if (a.realized) {
+        const float y = on ? a.realized[(size_t)p * a.N + i] : 0.0f;
+        const float r = np_expf(y) - 1.0f;
+        port = group_sum_bt<GL>(on ? 0.0 + tgi * (double)r : 0.0);
+        value *= (1.0 + port);
+        double denom = 1.0 + port;
+        if (fabs(denom) < 1e-8) denom = 1e-8;
+        const float g = 1.0f + (np_expf(y) - 1.0f);
+        if (on) w[i] = tgi * (double)g / denom;
+    } else {
+        if (on) w[i] = tgi;
+    }
+    if (i == 0) {
+        a.value[p] = value;
+        double* h = a.hist + ((size_t)p * a.S + a.k) * 4;
+        h[0] = value;
+        h[1] = port;
+        h[2] = turnover;
+        h[3] = cost;
+    }
+}
+
 }  // namespace bt
 }  // namespace kmpc

@@ -359,8 +359,9 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
 
 // kmpc_backtest_run: a path-persistent kernel exists for the shapes whose per-step batch of P
 // windows kmpc_solve sends to a float64 constant-case register kernel (case 7: no short, cost and
-// cap; H = 10 or 5, N <= 256, one window per workgroup — not the packed N <= 32 kernels, not the
-// mixed pair): the persistent kernel runs that kernel's window body, so the steps match it
+// cap; H = 10 or 5 with 32 < N <= 256, one window per workgroup; and the packed N <= 32 kernels
+// with H = 2, 5 or 10, one path per lane group — not the mixed pair): the persistent kernel runs
+// that kernel's window body, so the steps match it
 int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd, int step0, int n_steps,
                         const float* yhat, const float* realized, int n_real, double* weights, double* value,
                         double* hist, double* target, int* status, double* obj, hipStream_t stream) {
@@ -369,9 +370,10 @@ int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd,
     SolveArgs a = make_args(&d);
     const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
     const bool packed = a.path != KMPC_PATH_REGISTER_UNPACKED && a.N <= 32 && a.H <= 10;
-    if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || packed || !fl7 || a.N > 256 ||
-        (a.H != 10 && a.H != 5))
+    if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || !fl7 || a.N > 256)
         return KMPC_ERR_UNSUPPORTED;
+    // (the packed kernels exist for H = 2, 5, 10 — launch_ipm_packed's HM, exact H only)
+    if (packed ? (a.H != 2 && a.H != 5 && a.H != 10) : (a.H != 10 && a.H != 5)) return KMPC_ERR_UNSUPPORTED;
     if (a.path != KMPC_PATH_AUTO && a.path != KMPC_PATH_REGISTER && a.path != KMPC_PATH_REGISTER_UNPACKED)
         return KMPC_ERR_UNSUPPORTED;
     const int nt = 64 * ((a.N + 63) / 64);
@@ -381,6 +383,12 @@ int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd,
     if (bd->P == 0 || n_steps == 0) return KMPC_OK;
     a.wout = target; a.status = status; a.obj = obj; a.iters = nullptr; a.trace = nullptr;
     a.yhat = yhat; a.wp = weights;
+#ifndef KMPC_DEV_ONLY_H10
+    if (packed) {
+        const auto fn = a.H == 2 ? launch_bt_run_packed<2> : (a.H == 5 ? launch_bt_run_packed<5> : launch_bt_run_packed<10>);
+        return fn(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value, hist, stream);
+    }
+#endif
     if (a.H == 10 && nt == 128 && a.N < QL_CS)
         return launch_bt_run_c3(a, n_steps, n_real, yhat, realized, step0, bd->S, bd->cost_coeff, weights, value,
                                 hist, stream);

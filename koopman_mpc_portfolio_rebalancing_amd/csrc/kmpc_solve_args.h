@@ -55,6 +55,10 @@ int launch_bt_run_c3(const SolveArgs& a, int n_steps, int n_real, const float* y
 template <int HM>
 int launch_bt_run_case(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
                        int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream);
+// ... and of the packed shapes (N <= 32, H = HM, one lane group per path; kmpc_solve_p*.hip)
+template <int HM>
+int launch_bt_run_packed(const SolveArgs& a, int n_steps, int n_real, const float* yhat, const float* realized,
+                         int step0, int S, double c, double* weights, double* value, double* hist, hipStream_t stream);
 // packed small-window kernels, 64 / GL windows per wave (kmpc_solve_p*.hip); KMPC_ERR_UNSUPPORTED
 // outside N <= 32, 3 H <= 32
 template <int HM>

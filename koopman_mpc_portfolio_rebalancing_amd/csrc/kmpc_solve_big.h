@@ -94,8 +94,18 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state;
 // DS holds P bs, the s right-hand side already scaled by P; RC* hold the corrector's targets
 // without the centring term -smu, which every reader subtracts)
+// (A_W2: the second buffer of w — the best iterate stays in one while the iteration goes on in
+// the other, KMPC_BIG_RECFOLD)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
-             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, N_ARR };
+             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, A_W2, N_ARR };
+// The best iterate's record folded into the iterate update: instead of a
+// sweep per improving iteration that copies W to the output and sums ||w_t - w_{t-1}||_1, the update
+// sweep sums that norm of the new iterate with its period sums (a fourth slot per period), and w is
+// double-buffered in the slab: an improving iterate just marks its buffer as the best, and the next
+// update writes the other one; the output is copied once, after the loop. Same iterates, same W.
+#ifndef KMPC_BIG_RECFOLD
+#define KMPC_BIG_RECFOLD 1
+#endif
 
 __host__ __device__ inline size_t slab_doubles(int HM, int NP) {
     return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
@@ -112,6 +122,10 @@ struct BigArgs {
 template <int HM, int NW = NWX>
 constexpr int fx_doubles() { return KP * HM + HM + NW * HM; }
 
+// reduction slots per wave: the Schur width, or the update's four sums per period
+template <int HM>
+constexpr int rk() { return (KMPC_BIG_RECFOLD && 4 * HM > KP) ? 4 * HM : KP; }
+
 // (allocated as LDS of bs_bytes<HM>(waves): red is the last member and only the block's waves'
 // rows of it exist)
 template <int HM>
@@ -119,7 +133,7 @@ struct BigShared {
     double G[G_DOUBLES];         // Schur matrix (lower triangle), then L (unit lower, strictly below)
     double gid[KP];              // 1 / D of G = L D L^T
     double q[KP];                // Schur solution (period-major index 3t + type)
-    double tot[KP];              // block-reduction totals (slots < 3 HM <= 63)
+    double tot[rk<HM>()];        // block-reduction totals (slots < 3 HM <= 63; 4 HM with KMPC_BIG_RECFOLD)
     double sc[2][NWX][2];        // per-wave partials of scalar reductions (alternating)
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
@@ -127,12 +141,13 @@ struct BigShared {
     double isp1[HM];   // 1 / (1 + gamma SP), SP = sum_i P (rho = gamma isp1)
     double pxa[HM];    // the direction's px summed over its solves: ds = P (DS - rho pxa), sum_i ds = pxa isp1
     double lsc[HM];    // log S_t of a period run on R / S_t (tiny gross returns), else 0
+    double l1c[HM];    // ||w_t - w_{t-1}||_1 of the current iterate (KMPC_BIG_RECFOLD: the update's fourth slot)
     int flag;
-    double red[NWX][KP];         // per-wave partial slots of a period reduction (rows < waves)
+    double red[NWX][rk<HM>()];   // per-wave partial slots of a period reduction (rows < waves)
 };
 // LDS doubles of a BigShared whose blocks have nw waves (the red rows past nw cut off)
 template <int HM>
-constexpr int bs_doubles(int nw) { return (int)((sizeof(BigShared<HM>) - sizeof(double) * (NWX - nw) * KP + 7) / 8); }
+constexpr int bs_doubles(int nw) { return (int)((sizeof(BigShared<HM>) - sizeof(double) * (NWX - nw) * rk<HM>() + 7) / 8); }
 
 // state of one (t, i) with its slack-derived quantities (recomputed, never stored)
 struct St {
@@ -195,6 +210,8 @@ struct Win {
     Case<FL> cs;
     double tau, isig, irsig, cs_c, wpi;
     int sbuf;
+    int aw = A_W;                // the buffer of w holding the current iterate (A_W / A_W2)
+    int abest = -1;              // ... and the best iterate (KMPC_BIG_RECFOLD), -1: none yet
     __amdgpu_buffer_rsrc_t rs;   // the slab (wave-uniform base and size)
     unsigned vo;                 // i * 8
     // fused solves (>= 512-thread blocks): LDS block [Gv: KP x HM][cv: HM][pxr: NWX x HM] (fx_doubles);
@@ -239,7 +256,7 @@ struct Win {
     }
     __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
     __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
-    __device__ __forceinline__ double wprev(int t) const { return t ? at(A_W, t - 1) : wpi; }
+    __device__ __forceinline__ double wprev(int t) const { return t ? at(aw, t - 1) : wpi; }
 
     // the stored state of (t, i) and the direction / targets the step, update and corrector
     // sweeps read with it: loaded one period ahead of its use, so that a wave keeps the next
@@ -250,7 +267,7 @@ struct Win {
     // dir: + DW, DS; rc: + RC1..RC3; rr: + R0, R1 (a refinement pass's right-hand side)
     __device__ __forceinline__ Pre pre(int t, bool dir = true, bool rc = true, bool rr = false) const {
         Pre p{};
-        p.w = at(A_W, t);
+        p.w = at(aw, t);
         p.s = at(A_S, t);
         p.l1 = at(A_L1, t);
         p.l2 = at(A_L2, t);
@@ -273,7 +290,7 @@ struct Win {
     }
     __device__ __forceinline__ St st(int t, double wp) const {
         St e;
-        e.w = at(A_W, t);
+        e.w = at(aw, t);
         e.s = at(A_S, t);
         e.l1 = at(A_L1, t);
         e.l2 = at(A_L2, t);
@@ -403,6 +420,7 @@ __device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
         sh.rg4[t] = (W.ht() && on) ? W.tau - ss - sh.z4[t] : 0.0;
         sh.rc4[t] = (W.ht() && on) ? sh.z4[t] * sh.l4[t] : 0.0;
         sh.iz4[t] = 1.0 / sh.z4[t];
+        if (KMPC_BIG_RECFOLD) sh.l1c[t] = on ? sh.tot[3 * W.H + t] : 0.0;
         if (t == 0) sh.flag = 0;
     }
     __syncthreads();
@@ -411,18 +429,23 @@ __device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
 // (1) period sums R.w, 1'w, 1's -> den, iden, rp, rg4, rc4, iz4, rw (period owners)
 template <int HM, int FL>
 __device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
+    double wprev = W.wpi;
     for (int t = 0; t < W.H; ++t) {
         double mw = 0.0, w = 0.0, s = 0.0;
         if (W.act) {
-            w = W.at(A_W, t);
+            w = W.at(W.aw, t);
             mw = W.mload(t) * w;
             s = W.at(A_S, t);
         }
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, w);
         W.slot(3 * t + 2, s);
+        if (KMPC_BIG_RECFOLD) {
+            W.slot(3 * W.H + t, W.act ? fabs(w - wprev) : 0.0);
+            wprev = w;
+        }
     }
-    W.finish(3 * W.H);
+    W.finish((KMPC_BIG_RECFOLD ? 4 : 3) * W.H);
     sums_owner(W);
 }
 
@@ -517,12 +540,12 @@ template <int HM, int FL>
 __device__ __forceinline__ void ph_record(Win<HM, FL>& W, double* wout, int tw) {
     auto& sh = W.sh;
     double wprev = W.wpi, wn = 0.0;
-    if (W.act) wn = W.at(A_W, 0);
+    if (W.act) wn = W.at(W.aw, 0);
     for (int t = 0; t < W.H; ++t) {
         double v = 0.0;
         if (W.act) {
             const double w = wn;
-            if (t + 1 < W.H) wn = W.at(A_W, t + 1);
+            if (t + 1 < W.H) wn = W.at(W.aw, t + 1);
             if (t < tw) wout[t * W.N + W.i] = w;
             v = fabs(w - wprev);
             wprev = w;
@@ -1336,7 +1359,9 @@ template <int HM, int FL>
 __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double smu) {
     auto& sh = W.sh;
     const int H = W.H;
-    double wprev = W.wpi, dwp = 0.0;
+    double wprev = W.wpi, dwp = 0.0, wnp = W.wpi;
+    // the new iterate goes to the buffer that does not hold the best one (in place otherwise)
+    const int tgt = (KMPC_BIG_RECFOLD && W.aw == W.abest) ? (W.aw == A_W ? A_W2 : A_W) : W.aw;
     typename Win<HM, FL>::Pre pn{}, pn2{};
     if (W.act) {
         pn = W.pre(0);
@@ -1363,15 +1388,20 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
             W.at(A_L3, t) = e.l3 + step * dl3;
             wn = e.w + step * dw;
             sn = e.s + step * ds;
-            W.at(A_W, t) = wn;
+            W.at(tgt, t) = wn;
             W.at(A_S, t) = sn;
             mw = e.m * wn;
         }
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, wn);
         W.slot(3 * t + 2, sn);
+        if (KMPC_BIG_RECFOLD) {
+            W.slot(3 * H + t, W.act ? fabs(wn - wnp) : 0.0);   // ||w_t - w_{t-1}||_1 of the new iterate
+            wnp = wn;
+        }
     }
-    W.finish(3 * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
+    W.aw = tgt;
+    W.finish((KMPC_BIG_RECFOLD ? 4 : 3) * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
     if (threadIdx.x < HM && (int)threadIdx.x < H) {
         const int t = threadIdx.x;
         sh.z4[t] += step * sh.dz4[t];
@@ -1408,7 +1438,17 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         if (!domain_ok || !isfinite(merit)) break;
         if (merit < best) {
             best = merit;
-            ph_record(W, wout, tw);
+            if (KMPC_BIG_RECFOLD) {
+                // this iterate is the answer so far: its buffer of w is kept (ph_update writes the
+                // other), its period totals for problem.value are copied (owners; read after the loop)
+                W.abest = W.aw;
+                if (threadIdx.x < HM) {
+                    sh.best_rw[threadIdx.x] = sh.rw[threadIdx.x];
+                    sh.best_l1[threadIdx.x] = sh.l1c[threadIdx.x];
+                }
+            } else {
+                ph_record(W, wout, tw);
+            }
         } else if (best < 1e-6 && merit > 1e4 * best) {
             break;   // numerical breakdown after convergence: keep the best iterate
         }
@@ -1460,6 +1500,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     const int N = a.N, H = a.H, i = threadIdx.x;
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        W.aw = A_W;
+        W.abest = -1;
         const double* wp = a.wp + (size_t)b * N;
         const float* yh = a.yhat + (size_t)b * H * N;
         double* wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
@@ -1548,7 +1590,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                     if (W.act) {
                         const double d = w0 - (t ? w0 : W.wpi);
                         s = hs ? fabs(d) + 1.0 / N : 0.0;
-                        W.at(A_W, t) = w0;
+                        W.at(A_W, t) = w0;   // (W.aw = A_W at every window's start)
                         W.at(A_S, t) = s;
                         W.at(A_L1, t) = hw ? 1.0 : 0.0;
                         W.at(A_L2, t) = hs ? 1.0 : 0.0;
@@ -1568,6 +1610,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                 const double inv_ncon = 1.0 / (ncon > 0 ? ncon : 1);
                 double best = 1e300, min_pr = 1e300;
                 it = ipm_iterate(W, wout, tw, inv_ncon, best, min_pr, b);
+                // W of the best iterate to the output (KMPC_BIG_RECFOLD: once, from its buffer)
+                if (KMPC_BIG_RECFOLD && W.abest >= 0 && W.act)
+                    for (int t = 0; t < tw; ++t) wout[t * N + i] = W.at(W.abest, t);
                 __syncthreads();   // sh.best_* of the best iterate visible
                 if (best < 1e300) {
                     double f = 0.0;

@@ -8,7 +8,7 @@
 #include "kmpc_bt_run.h"
 
 #ifndef KMPC_REG_HANDOFF_ON   // ipm_mixed_kernel's handoff: 2 LDS, 1 registers, 0 the warm record in HBM
-#define KMPC_REG_HANDOFF_ON 2
+#define KMPC_REG_HANDOFF_ON 1
 #endif
 
 namespace kmpc {

@@ -553,12 +553,6 @@ constexpr size_t cold_bytes() { return cold_in_lds<HM, MAXT, CS, QL, GL, FL, Rea
 
 // ---- shared state -------------------------------------------------------------------------------
 
-// lsolve's never-taken branch that steered the register allocation (r04: +2.8% on the float64 C3
-// solve); 0 drops it (dev A/B of VERDICT r05 item 8)
-#ifndef KMPC_LSOLVE_STEER
-#define KMPC_LSOLVE_STEER 1
-#endif
-
 template <int HM, int NWM, class Real = double>
 struct Shared {
     static constexpr int KM = 3 * HM;
@@ -580,7 +574,6 @@ struct Shared {
     Real den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM];
     Real rho[HM], sr[HM];
     Real sp[HM], isp1[HM];             // sum_i P per period; 1 / (1 + gamma SP) (rho = gamma isp1)
-    Real pxd[NWM][pow2_at_least(HM)];  // (read only by an untaken branch of lsolve: see there)
     Real rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
     Real best_rw[HM], best_l1[HM];   // per-period R.w and ||w_t - w_{t-1}||_1 of the best iterate
     Real lsc[HM];                    // log S_t of a period run on R / S_t (tiny gross returns), else 0
@@ -1040,21 +1033,6 @@ __device__ __forceinline__ void lsolve(const TH& T, Shared<HM, NWM, typename TH:
 #pragma unroll
             for (int t = 0; t < HM; ++t)
                 px[t] = t < H ? (-T.c - sh.l4[t] - (T.ht ? sh.lb5[t] * sh.iz4[t] : Real(0.0))) * sh.sp[t] : Real(0.0);
-        } else if (KMPC_LSOLVE_STEER && T.N < 0) {
-            // Never taken (N >= 1: the C ABI rejects the rest). Kept because this branch's presence
-            // changes the register allocation of the whole kernel: 46 -> 41 spilled VGPRs and +2.8%
-            // on the C3 solve, measured r04 (tools/ab_run.sh, two repeats; the compiler drops a
-            // branch whose condition it can prove false, and then the gain is gone). A live use —
-            // the refinement solves' px reduced with the residual norm into sh.pxd — spilled 121
-            // VGPRs at the refinement loop's peak and was slower.
-#pragma unroll
-            for (int t = 0; t < HM; ++t) {
-                Real v = sh.pxd[0][t];
-#pragma unroll
-                for (int q = 1; q < NWM; ++q)
-                    if (q < R.nw) v += sh.pxd[q][t];
-                px[t] = t < H ? v - (T.ht ? sh.lb5[t] * sh.iz4[t] : Real(0.0)) * sh.sp[t] : Real(0.0);
-            }
         } else {
 #pragma unroll
             for (int t = 0; t < HM; ++t) px[t] = T.P[t] * bs[t];

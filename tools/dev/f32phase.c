@@ -152,7 +152,9 @@ int API(kmpc_phase)(int N, int H, const double* wp, const float* yhat, double c,
         }
         {
             const int nr = W.n_refine;
-            if (mu > (real)1e-6) W.n_refine = 0;
+            /* dev knob: F32PH_REFMU refines the corrector from that mu (default 1e-6, the kernels') */
+            const char* e = getenv("F32PH_REFMU");
+            if (mu > (real)(e ? atof(e) : 1e-6)) W.n_refine = 0;
             newton(&W);
             W.n_refine = nr;
         }
