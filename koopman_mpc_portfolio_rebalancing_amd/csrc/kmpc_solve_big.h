@@ -98,14 +98,19 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // the other, KMPC_BIG_RECFOLD)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
              A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, A_W2, N_ARR };
-// The best iterate's record folded into the iterate update: instead of a
-// sweep per improving iteration that copies W to the output and sums ||w_t - w_{t-1}||_1, the update
-// sweep sums that norm of the new iterate with its period sums (a fourth slot per period), and w is
-// double-buffered in the slab: an improving iterate just marks its buffer as the best, and the next
-// update writes the other one; the output is copied once, after the loop. Same iterates, same W.
+// The best iterate's record folded into other sweeps, instead of a sweep per
+// improving iteration that copies W to the output and sums ||w_t - w_{t-1}||_1 (ph_record, mode 0):
+//   3 (default): the factor sweep, which reads w_t and w_{t-1} anyway, sums ||d_t||_1 into a second
+//     slot per period; the update sweep that replaces an improving iterate writes its W (t < tw)
+//     from the w it loads anyway; the loop's last iterate, if best, goes out after the loop;
+//   1: w double-buffered in the slab (an improving iterate marks its buffer, the next update writes
+//     the other one; one copy after the loop) and the norm as a fourth slot of the update's sums —
+//     the run-time buffer index and the slot cost 14 more spilled VGPRs: C5 61.7 -> 64.2 ms (r06).
+// Same iterates, same W.
 #ifndef KMPC_BIG_RECFOLD
-#define KMPC_BIG_RECFOLD 1
+#define KMPC_BIG_RECFOLD 3
 #endif
+static_assert(KMPC_BIG_RECFOLD == 0 || KMPC_BIG_RECFOLD == 1 || KMPC_BIG_RECFOLD == 3, "record fold mode");
 
 __host__ __device__ inline size_t slab_doubles(int HM, int NP) {
     return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
@@ -124,7 +129,7 @@ constexpr int fx_doubles() { return KP * HM + HM + NW * HM; }
 
 // reduction slots per wave: the Schur width, or the update's four sums per period
 template <int HM>
-constexpr int rk() { return (KMPC_BIG_RECFOLD && 4 * HM > KP) ? 4 * HM : KP; }
+constexpr int rk() { return (KMPC_BIG_RECFOLD == 1 && 4 * HM > KP) ? 4 * HM : KP; }
 
 // (allocated as LDS of bs_bytes<HM>(waves): red is the last member and only the block's waves'
 // rows of it exist)
@@ -210,8 +215,11 @@ struct Win {
     Case<FL> cs;
     double tau, isig, irsig, cs_c, wpi;
     int sbuf;
-    int aw = A_W;                // the buffer of w holding the current iterate (A_W / A_W2)
+    int aw = A_W;                // the buffer of w holding the current iterate (A_W / A_W2; mode 1)
     int abest = -1;              // ... and the best iterate (KMPC_BIG_RECFOLD), -1: none yet
+    bool rec = false;            // mode 3: the current iterate is the best so far, its W not yet output
+    double* wout = nullptr;      // mode 3: the window's output rows (t < tw)
+    int tw = 1;
     __amdgpu_buffer_rsrc_t rs;   // the slab (wave-uniform base and size)
     unsigned vo;                 // i * 8
     // fused solves (>= 512-thread blocks): LDS block [Gv: KP x HM][cv: HM][pxr: NWX x HM] (fx_doubles);
@@ -256,7 +264,9 @@ struct Win {
     }
     __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
     __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
-    __device__ __forceinline__ double wprev(int t) const { return t ? at(aw, t - 1) : wpi; }
+    // the buffer of w holding the current iterate (a run-time index only with the double buffer)
+    __device__ __forceinline__ int wa() const { return KMPC_BIG_RECFOLD == 1 ? aw : (int)A_W; }
+    __device__ __forceinline__ double wprev(int t) const { return t ? at(wa(), t - 1) : wpi; }
 
     // the stored state of (t, i) and the direction / targets the step, update and corrector
     // sweeps read with it: loaded one period ahead of its use, so that a wave keeps the next
@@ -267,7 +277,7 @@ struct Win {
     // dir: + DW, DS; rc: + RC1..RC3; rr: + R0, R1 (a refinement pass's right-hand side)
     __device__ __forceinline__ Pre pre(int t, bool dir = true, bool rc = true, bool rr = false) const {
         Pre p{};
-        p.w = at(aw, t);
+        p.w = at(wa(), t);
         p.s = at(A_S, t);
         p.l1 = at(A_L1, t);
         p.l2 = at(A_L2, t);
@@ -290,7 +300,7 @@ struct Win {
     }
     __device__ __forceinline__ St st(int t, double wp) const {
         St e;
-        e.w = at(aw, t);
+        e.w = at(wa(), t);
         e.s = at(A_S, t);
         e.l1 = at(A_L1, t);
         e.l2 = at(A_L2, t);
@@ -420,7 +430,7 @@ __device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
         sh.rg4[t] = (W.ht() && on) ? W.tau - ss - sh.z4[t] : 0.0;
         sh.rc4[t] = (W.ht() && on) ? sh.z4[t] * sh.l4[t] : 0.0;
         sh.iz4[t] = 1.0 / sh.z4[t];
-        if (KMPC_BIG_RECFOLD) sh.l1c[t] = on ? sh.tot[3 * W.H + t] : 0.0;
+        if (KMPC_BIG_RECFOLD == 1) sh.l1c[t] = on ? sh.tot[3 * W.H + t] : 0.0;
         if (t == 0) sh.flag = 0;
     }
     __syncthreads();
@@ -433,19 +443,19 @@ __device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
     for (int t = 0; t < W.H; ++t) {
         double mw = 0.0, w = 0.0, s = 0.0;
         if (W.act) {
-            w = W.at(W.aw, t);
+            w = W.at(W.wa(), t);
             mw = W.mload(t) * w;
             s = W.at(A_S, t);
         }
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, w);
         W.slot(3 * t + 2, s);
-        if (KMPC_BIG_RECFOLD) {
+        if (KMPC_BIG_RECFOLD == 1) {
             W.slot(3 * W.H + t, W.act ? fabs(w - wprev) : 0.0);
             wprev = w;
         }
     }
-    W.finish((KMPC_BIG_RECFOLD ? 4 : 3) * W.H);
+    W.finish((KMPC_BIG_RECFOLD == 1 ? 4 : 3) * W.H);
     sums_owner(W);
 }
 
@@ -472,7 +482,7 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
         pi = W1c + Ec;
     }
     for (int t = 0; t < H; ++t) {
-        double P = 0.0;
+        double P = 0.0, ad = 0.0;
         if (W.act) {
             const bool nx = t + 1 < H;
             St nxt = cur;
@@ -491,6 +501,7 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             mu_l += r1 + r2 + r3;
             rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
             P = cur.P;
+            ad = fabs(cur.d);
             W.fat(A_P, t) = cur.P;
             W.fat(A_BP, t) = cur.bma * cur.P;
             // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
@@ -511,6 +522,7 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             cur = nxt;
         }
         W.slot(t, P);
+        if (KMPC_BIG_RECFOLD >= 2) W.slot(H + t, ad);   // ||w_t - w_{t-1}||_1 of this iterate
     }
     if (W.act) {
         // the Schur generators' centred pi_{H-1} (ph_gram runs its pi recursion backward from it):
@@ -520,10 +532,11 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
         const int e = pe + e2;
         W.at(A_X, 0) = ldexp(m, e - e / 2);
     }
-    W.finish(H);
+    W.finish(KMPC_BIG_RECFOLD >= 2 ? 2 * H : H);
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
         const double st = t < H ? sh.tot[t] : 0.0;
+        if (KMPC_BIG_RECFOLD >= 2) sh.l1c[t] = t < H ? sh.tot[H + t] : 0.0;
         const double ga = (ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
         const double i1 = 1.0 / (1.0 + ga * st);
         sh.rho[t] = (ht && t < H) ? ga * i1 : 0.0;
@@ -540,12 +553,12 @@ template <int HM, int FL>
 __device__ __forceinline__ void ph_record(Win<HM, FL>& W, double* wout, int tw) {
     auto& sh = W.sh;
     double wprev = W.wpi, wn = 0.0;
-    if (W.act) wn = W.at(W.aw, 0);
+    if (W.act) wn = W.at(W.wa(), 0);
     for (int t = 0; t < W.H; ++t) {
         double v = 0.0;
         if (W.act) {
             const double w = wn;
-            if (t + 1 < W.H) wn = W.at(W.aw, t + 1);
+            if (t + 1 < W.H) wn = W.at(W.wa(), t + 1);
             if (t < tw) wout[t * W.N + W.i] = w;
             v = fabs(w - wprev);
             wprev = w;
@@ -1361,7 +1374,7 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
     const int H = W.H;
     double wprev = W.wpi, dwp = 0.0, wnp = W.wpi;
     // the new iterate goes to the buffer that does not hold the best one (in place otherwise)
-    const int tgt = (KMPC_BIG_RECFOLD && W.aw == W.abest) ? (W.aw == A_W ? A_W2 : A_W) : W.aw;
+    const int tgt = (KMPC_BIG_RECFOLD == 1 && W.aw == W.abest) ? (W.aw == A_W ? A_W2 : A_W) : W.wa();
     typename Win<HM, FL>::Pre pn{}, pn2{};
     if (W.act) {
         pn = W.pre(0);
@@ -1379,6 +1392,7 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
             }
             const St e = W.st(p, wprev);
             wprev = e.w;
+            if (KMPC_BIG_RECFOLD == 3 && W.rec && t < W.tw) W.wout[t * W.N + W.i] = e.w;   // the best iterate's W
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
@@ -1395,13 +1409,14 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, wn);
         W.slot(3 * t + 2, sn);
-        if (KMPC_BIG_RECFOLD) {
+        if (KMPC_BIG_RECFOLD == 1) {
             W.slot(3 * H + t, W.act ? fabs(wn - wnp) : 0.0);   // ||w_t - w_{t-1}||_1 of the new iterate
             wnp = wn;
         }
     }
     W.aw = tgt;
-    W.finish((KMPC_BIG_RECFOLD ? 4 : 3) * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
+    W.rec = false;
+    W.finish((KMPC_BIG_RECFOLD == 1 ? 4 : 3) * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
     if (threadIdx.x < HM && (int)threadIdx.x < H) {
         const int t = threadIdx.x;
         sh.z4[t] += step * sh.dz4[t];
@@ -1439,9 +1454,11 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         if (merit < best) {
             best = merit;
             if (KMPC_BIG_RECFOLD) {
-                // this iterate is the answer so far: its buffer of w is kept (ph_update writes the
-                // other), its period totals for problem.value are copied (owners; read after the loop)
+                // this iterate is the answer so far: its buffer of w is kept (mode 1: ph_update
+                // writes the other) or its W goes out in the update sweep that replaces it (mode 3);
+                // its period totals for problem.value are copied (owners; read after the loop)
                 W.abest = W.aw;
+                W.rec = true;
                 if (threadIdx.x < HM) {
                     sh.best_rw[threadIdx.x] = sh.rw[threadIdx.x];
                     sh.best_l1[threadIdx.x] = sh.l1c[threadIdx.x];
@@ -1502,6 +1519,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         W.aw = A_W;
         W.abest = -1;
+        W.rec = false;
+        W.wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
+        W.tw = a.return_full ? H : 1;
         const double* wp = a.wp + (size_t)b * N;
         const float* yh = a.yhat + (size_t)b * H * N;
         double* wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
@@ -1611,8 +1631,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                 double best = 1e300, min_pr = 1e300;
                 it = ipm_iterate(W, wout, tw, inv_ncon, best, min_pr, b);
                 // W of the best iterate to the output (KMPC_BIG_RECFOLD: once, from its buffer)
-                if (KMPC_BIG_RECFOLD && W.abest >= 0 && W.act)
+                if (KMPC_BIG_RECFOLD == 1 && W.abest >= 0 && W.act)
                     for (int t = 0; t < tw; ++t) wout[t * N + i] = W.at(W.abest, t);
+                if (KMPC_BIG_RECFOLD == 3 && W.rec && W.act)   // (the loop ended on the best iterate)
+                    for (int t = 0; t < tw; ++t) wout[t * N + i] = W.at(A_W, t);
                 __syncthreads();   // sh.best_* of the best iterate visible
                 if (best < 1e300) {
                     double f = 0.0;

@@ -83,7 +83,9 @@ def test_argument_errors_need_no_gpu():
     assert run(0, 0, None, None, 0) == 0
     sd.H = 7                                                  # another horizon: no persistent kernel
     assert run(0, 0, None, None, 0) == -2
-    sd.H, sd.N, btr.N = 5, 20, 20                             # N <= 32: the packed kernels, no persistent form
+    sd.H, sd.N, btr.N = 5, 20, 20                             # N <= 32: the packed kernels' persistent form
+    assert run(0, 0, None, None, 0) == 0
+    sd.H = 3                                                  # a ragged packed horizon: no persistent form
     assert run(0, 0, None, None, 0) == -2
     sd.N, btr.N = 100, 100
     sd.H, sd.cost_coeff = 10, -1.0                            # the solve's own checks apply

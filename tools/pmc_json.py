@@ -50,7 +50,7 @@ f32_db = os.environ.get("F32_DB")   # optional pass with the float32 VALU counte
 d = {"kernel": kernel_name(fetch_db), "windows_per_launch": B,
      "fetch_bytes_per_window": 2 * 1024 * mean(fetch_db, "FETCH_SIZE") / B,
      "write_bytes_per_window": 1024 * mean(write_db, "WRITE_SIZE") / B,
-     "source": "rocprofv3 --pmc passes of `python bench.py --cpu-seconds 0 --steps 3 --warmup 1` (tools/gpu_round5.sh)"}
+     "source": "rocprofv3 --pmc passes of `python bench.py --cpu-seconds 0 --steps 3 --warmup 1 --headline-only` (tools/gpu_round6.sh)"}
 ins = {c: mean(f64_db, c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
                                     "SQ_INSTS_VALU_TRANS_F64", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
                                     "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU")}
