@@ -94,23 +94,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // so that the Newton passes read 1-2 arrays instead of recomputing them from the whole state;
 // DS holds P bs, the s right-hand side already scaled by P; RC* hold the corrector's targets
 // without the centring term -smu, which every reader subtracts)
-// (A_W2: the second buffer of w — the best iterate stays in one while the iteration goes on in
-// the other, KMPC_BIG_RECFOLD)
 enum : int { A_W, A_S, A_L1, A_L2, A_L3, A_M, A_LR, A_IDD, A_RC1, A_RC2, A_RC3, A_DW, A_DS,
-             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, A_W2, N_ARR };
-// The best iterate's record folded into other sweeps, instead of a sweep per
-// improving iteration that copies W to the output and sums ||w_t - w_{t-1}||_1 (ph_record, mode 0):
-//   3 (default): the factor sweep, which reads w_t and w_{t-1} anyway, sums ||d_t||_1 into a second
-//     slot per period; the update sweep that replaces an improving iterate writes its W (t < tw)
-//     from the w it loads anyway; the loop's last iterate, if best, goes out after the loop;
-//   1: w double-buffered in the slab (an improving iterate marks its buffer, the next update writes
-//     the other one; one copy after the loop) and the norm as a fourth slot of the update's sums —
-//     the run-time buffer index and the slot cost 14 more spilled VGPRs: C5 61.7 -> 64.2 ms (r06).
-// Same iterates, same W.
-#ifndef KMPC_BIG_RECFOLD
-#define KMPC_BIG_RECFOLD 3
-#endif
-static_assert(KMPC_BIG_RECFOLD == 0 || KMPC_BIG_RECFOLD == 1 || KMPC_BIG_RECFOLD == 3, "record fold mode");
+             A_BW, A_BS, A_X, A_Y, A_R0, A_R1, A_P, A_BP, N_ARR };
 
 __host__ __device__ inline size_t slab_doubles(int HM, int NP) {
     return (size_t)N_ARR * HM * NP + 2 * (size_t)KP * NP;
@@ -127,10 +112,6 @@ struct BigArgs {
 template <int HM, int NW = NWX>
 constexpr int fx_doubles() { return KP * HM + HM + NW * HM; }
 
-// reduction slots per wave: the Schur width, or the update's four sums per period
-template <int HM>
-constexpr int rk() { return (KMPC_BIG_RECFOLD == 1 && 4 * HM > KP) ? 4 * HM : KP; }
-
 // (allocated as LDS of bs_bytes<HM>(waves): red is the last member and only the block's waves'
 // rows of it exist)
 template <int HM>
@@ -138,7 +119,7 @@ struct BigShared {
     double G[G_DOUBLES];         // Schur matrix (lower triangle), then L (unit lower, strictly below)
     double gid[KP];              // 1 / D of G = L D L^T
     double q[KP];                // Schur solution (period-major index 3t + type)
-    double tot[rk<HM>()];        // block-reduction totals (slots < 3 HM <= 63; 4 HM with KMPC_BIG_RECFOLD)
+    double tot[KP];              // block-reduction totals (slots < 3 HM <= 63)
     double sc[2][NWX][2];        // per-wave partials of scalar reductions (alternating)
     double den[HM], iden[HM], rp[HM], rg4[HM], z4[HM], iz4[HM], l4[HM], nu[HM], rho[HM], sr[HM];
     double rc4[HM], b5[HM], b6[HM], lb5[HM], lb6[HM], dnu[HM], dz4[HM], dl4[HM];
@@ -146,13 +127,12 @@ struct BigShared {
     double isp1[HM];   // 1 / (1 + gamma SP), SP = sum_i P (rho = gamma isp1)
     double pxa[HM];    // the direction's px summed over its solves: ds = P (DS - rho pxa), sum_i ds = pxa isp1
     double lsc[HM];    // log S_t of a period run on R / S_t (tiny gross returns), else 0
-    double l1c[HM];    // ||w_t - w_{t-1}||_1 of the current iterate (KMPC_BIG_RECFOLD: the update's fourth slot)
     int flag;
-    double red[NWX][rk<HM>()];   // per-wave partial slots of a period reduction (rows < waves)
+    double red[NWX][KP];         // per-wave partial slots of a period reduction (rows < waves)
 };
 // LDS doubles of a BigShared whose blocks have nw waves (the red rows past nw cut off)
 template <int HM>
-constexpr int bs_doubles(int nw) { return (int)((sizeof(BigShared<HM>) - sizeof(double) * (NWX - nw) * rk<HM>() + 7) / 8); }
+constexpr int bs_doubles(int nw) { return (int)((sizeof(BigShared<HM>) - sizeof(double) * (NWX - nw) * KP + 7) / 8); }
 
 // state of one (t, i) with its slack-derived quantities (recomputed, never stored)
 struct St {
@@ -215,11 +195,6 @@ struct Win {
     Case<FL> cs;
     double tau, isig, irsig, cs_c, wpi;
     int sbuf;
-    int aw = A_W;                // the buffer of w holding the current iterate (A_W / A_W2; mode 1)
-    int abest = -1;              // ... and the best iterate (KMPC_BIG_RECFOLD), -1: none yet
-    bool rec = false;            // mode 3: the current iterate is the best so far, its W not yet output
-    double* wout = nullptr;      // mode 3: the window's output rows (t < tw)
-    int tw = 1;
     __amdgpu_buffer_rsrc_t rs;   // the slab (wave-uniform base and size)
     unsigned vo;                 // i * 8
     // fused solves (>= 512-thread blocks): LDS block [Gv: KP x HM][cv: HM][pxr: NWX x HM] (fx_doubles);
@@ -264,9 +239,7 @@ struct Win {
     }
     __device__ __forceinline__ double* lg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)j * NP; }
     __device__ __forceinline__ double* rg(int j) const { return g + (size_t)N_ARR * HM * NP + (size_t)(KP + j) * NP; }
-    // the buffer of w holding the current iterate (a run-time index only with the double buffer)
-    __device__ __forceinline__ int wa() const { return KMPC_BIG_RECFOLD == 1 ? aw : (int)A_W; }
-    __device__ __forceinline__ double wprev(int t) const { return t ? at(wa(), t - 1) : wpi; }
+    __device__ __forceinline__ double wprev(int t) const { return t ? at(A_W, t - 1) : wpi; }
 
     // the stored state of (t, i) and the direction / targets the step, update and corrector
     // sweeps read with it: loaded one period ahead of its use, so that a wave keeps the next
@@ -277,7 +250,7 @@ struct Win {
     // dir: + DW, DS; rc: + RC1..RC3; rr: + R0, R1 (a refinement pass's right-hand side)
     __device__ __forceinline__ Pre pre(int t, bool dir = true, bool rc = true, bool rr = false) const {
         Pre p{};
-        p.w = at(wa(), t);
+        p.w = at(A_W, t);
         p.s = at(A_S, t);
         p.l1 = at(A_L1, t);
         p.l2 = at(A_L2, t);
@@ -300,7 +273,7 @@ struct Win {
     }
     __device__ __forceinline__ St st(int t, double wp) const {
         St e;
-        e.w = at(wa(), t);
+        e.w = at(A_W, t);
         e.s = at(A_S, t);
         e.l1 = at(A_L1, t);
         e.l2 = at(A_L2, t);
@@ -430,7 +403,6 @@ __device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
         sh.rg4[t] = (W.ht() && on) ? W.tau - ss - sh.z4[t] : 0.0;
         sh.rc4[t] = (W.ht() && on) ? sh.z4[t] * sh.l4[t] : 0.0;
         sh.iz4[t] = 1.0 / sh.z4[t];
-        if (KMPC_BIG_RECFOLD == 1) sh.l1c[t] = on ? sh.tot[3 * W.H + t] : 0.0;
         if (t == 0) sh.flag = 0;
     }
     __syncthreads();
@@ -439,23 +411,18 @@ __device__ __forceinline__ void sums_owner(Win<HM, FL>& W) {
 // (1) period sums R.w, 1'w, 1's -> den, iden, rp, rg4, rc4, iz4, rw (period owners)
 template <int HM, int FL>
 __device__ __forceinline__ void ph_sums(Win<HM, FL>& W) {
-    double wprev = W.wpi;
     for (int t = 0; t < W.H; ++t) {
         double mw = 0.0, w = 0.0, s = 0.0;
         if (W.act) {
-            w = W.at(W.wa(), t);
+            w = W.at(A_W, t);
             mw = W.mload(t) * w;
             s = W.at(A_S, t);
         }
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, w);
         W.slot(3 * t + 2, s);
-        if (KMPC_BIG_RECFOLD == 1) {
-            W.slot(3 * W.H + t, W.act ? fabs(w - wprev) : 0.0);
-            wprev = w;
-        }
     }
-    W.finish((KMPC_BIG_RECFOLD == 1 ? 4 : 3) * W.H);
+    W.finish(3 * W.H);
     sums_owner(W);
 }
 
@@ -482,7 +449,7 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
         pi = W1c + Ec;
     }
     for (int t = 0; t < H; ++t) {
-        double P = 0.0, ad = 0.0;
+        double P = 0.0;
         if (W.act) {
             const bool nx = t + 1 < H;
             St nxt = cur;
@@ -501,7 +468,6 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             mu_l += r1 + r2 + r3;
             rd = fmax(rd, fmax(fabs(rdw), fabs(rds)));
             P = cur.P;
-            ad = fabs(cur.d);
             W.fat(A_P, t) = cur.P;
             W.fat(A_BP, t) = cur.bma * cur.P;
             // LDL^T of Q = diag(W1) + D^T E D, cancellation-free pivots
@@ -522,7 +488,6 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
             cur = nxt;
         }
         W.slot(t, P);
-        if (KMPC_BIG_RECFOLD >= 2) W.slot(H + t, ad);   // ||w_t - w_{t-1}||_1 of this iterate
     }
     if (W.act) {
         // the Schur generators' centred pi_{H-1} (ph_gram runs its pi recursion backward from it):
@@ -532,11 +497,10 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
         const int e = pe + e2;
         W.at(A_X, 0) = ldexp(m, e - e / 2);
     }
-    W.finish(KMPC_BIG_RECFOLD >= 2 ? 2 * H : H);
+    W.finish(H);
     if (threadIdx.x < HM) {
         const int t = threadIdx.x;
         const double st = t < H ? sh.tot[t] : 0.0;
-        if (KMPC_BIG_RECFOLD >= 2) sh.l1c[t] = t < H ? sh.tot[H + t] : 0.0;
         const double ga = (ht && t < H) ? sh.l4[t] / sh.z4[t] : 0.0;
         const double i1 = 1.0 / (1.0 + ga * st);
         sh.rho[t] = (ht && t < H) ? ga * i1 : 0.0;
@@ -548,17 +512,20 @@ __device__ __forceinline__ void ph_factor(Win<HM, FL>& W, double& mu_l, double& 
 }
 
 // W (t < tw) of the current iterate to the output, and the per-period ||w_t - w_{t-1}||_1 and R.w
-// of this iterate (its objective is evaluated after the loop)
+// of this iterate (its objective is evaluated after the loop). (Folding this sweep into the update
+// or factor sweeps — w double-buffered in the slab, or W written by the update that replaces the
+// best iterate, the norm as an extra reduction slot — measured slower on C5: 61.7 -> 64.2 / 62.4 ms,
+// 60 -> 74 / 63 spilled VGPRs in the load-latency-bound sweeps; r06, commit 518ee52)
 template <int HM, int FL>
 __device__ __forceinline__ void ph_record(Win<HM, FL>& W, double* wout, int tw) {
     auto& sh = W.sh;
     double wprev = W.wpi, wn = 0.0;
-    if (W.act) wn = W.at(W.wa(), 0);
+    if (W.act) wn = W.at(A_W, 0);
     for (int t = 0; t < W.H; ++t) {
         double v = 0.0;
         if (W.act) {
             const double w = wn;
-            if (t + 1 < W.H) wn = W.at(W.wa(), t + 1);
+            if (t + 1 < W.H) wn = W.at(A_W, t + 1);
             if (t < tw) wout[t * W.N + W.i] = w;
             v = fabs(w - wprev);
             wprev = w;
@@ -1372,9 +1339,7 @@ template <int HM, int FL>
 __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double smu) {
     auto& sh = W.sh;
     const int H = W.H;
-    double wprev = W.wpi, dwp = 0.0, wnp = W.wpi;
-    // the new iterate goes to the buffer that does not hold the best one (in place otherwise)
-    const int tgt = (KMPC_BIG_RECFOLD == 1 && W.aw == W.abest) ? (W.aw == A_W ? A_W2 : A_W) : W.wa();
+    double wprev = W.wpi, dwp = 0.0;
     typename Win<HM, FL>::Pre pn{}, pn2{};
     if (W.act) {
         pn = W.pre(0);
@@ -1392,7 +1357,6 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
             }
             const St e = W.st(p, wprev);
             wprev = e.w;
-            if (KMPC_BIG_RECFOLD == 3 && W.rec && t < W.tw) W.wout[t * W.N + W.i] = e.w;   // the best iterate's W
             const double dw = p.dw, ds = W.dsv(t, e, p.ds), dd = dw - dwp;
             dwp = dw;
             double dl1, dl2, dl3;
@@ -1402,21 +1366,15 @@ __device__ __forceinline__ void ph_update(Win<HM, FL>& W, double step, double sm
             W.at(A_L3, t) = e.l3 + step * dl3;
             wn = e.w + step * dw;
             sn = e.s + step * ds;
-            W.at(tgt, t) = wn;
+            W.at(A_W, t) = wn;
             W.at(A_S, t) = sn;
             mw = e.m * wn;
         }
         W.slot(3 * t, mw);
         W.slot(3 * t + 1, wn);
         W.slot(3 * t + 2, sn);
-        if (KMPC_BIG_RECFOLD == 1) {
-            W.slot(3 * H + t, W.act ? fabs(wn - wnp) : 0.0);   // ||w_t - w_{t-1}||_1 of the new iterate
-            wnp = wn;
-        }
     }
-    W.aw = tgt;
-    W.rec = false;
-    W.finish((KMPC_BIG_RECFOLD == 1 ? 4 : 3) * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
+    W.finish(3 * H);   // (its first barrier: every ratio test has read z4 / l4 before the owners update them)
     if (threadIdx.x < HM && (int)threadIdx.x < H) {
         const int t = threadIdx.x;
         sh.z4[t] += step * sh.dz4[t];
@@ -1453,19 +1411,7 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
         if (!domain_ok || !isfinite(merit)) break;
         if (merit < best) {
             best = merit;
-            if (KMPC_BIG_RECFOLD) {
-                // this iterate is the answer so far: its buffer of w is kept (mode 1: ph_update
-                // writes the other) or its W goes out in the update sweep that replaces it (mode 3);
-                // its period totals for problem.value are copied (owners; read after the loop)
-                W.abest = W.aw;
-                W.rec = true;
-                if (threadIdx.x < HM) {
-                    sh.best_rw[threadIdx.x] = sh.rw[threadIdx.x];
-                    sh.best_l1[threadIdx.x] = sh.l1c[threadIdx.x];
-                }
-            } else {
-                ph_record(W, wout, tw);
-            }
+            ph_record(W, wout, tw);
         } else if (best < 1e-6 && merit > 1e4 * best) {
             break;   // numerical breakdown after convergence: keep the best iterate
         }
@@ -1517,11 +1463,6 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     const int N = a.N, H = a.H, i = threadIdx.x;
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
-        W.aw = A_W;
-        W.abest = -1;
-        W.rec = false;
-        W.wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
-        W.tw = a.return_full ? H : 1;
         const double* wp = a.wp + (size_t)b * N;
         const float* yh = a.yhat + (size_t)b * H * N;
         double* wout = a.wout + (size_t)b * (a.return_full ? H * N : N);
@@ -1610,7 +1551,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                     if (W.act) {
                         const double d = w0 - (t ? w0 : W.wpi);
                         s = hs ? fabs(d) + 1.0 / N : 0.0;
-                        W.at(A_W, t) = w0;   // (W.aw = A_W at every window's start)
+                        W.at(A_W, t) = w0;
                         W.at(A_S, t) = s;
                         W.at(A_L1, t) = hw ? 1.0 : 0.0;
                         W.at(A_L2, t) = hs ? 1.0 : 0.0;
@@ -1630,11 +1571,6 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                 const double inv_ncon = 1.0 / (ncon > 0 ? ncon : 1);
                 double best = 1e300, min_pr = 1e300;
                 it = ipm_iterate(W, wout, tw, inv_ncon, best, min_pr, b);
-                // W of the best iterate to the output (KMPC_BIG_RECFOLD: once, from its buffer)
-                if (KMPC_BIG_RECFOLD == 1 && W.abest >= 0 && W.act)
-                    for (int t = 0; t < tw; ++t) wout[t * N + i] = W.at(W.abest, t);
-                if (KMPC_BIG_RECFOLD == 3 && W.rec && W.act)   // (the loop ended on the best iterate)
-                    for (int t = 0; t < tw; ++t) wout[t * N + i] = W.at(A_W, t);
                 __syncthreads();   // sh.best_* of the best iterate visible
                 if (best < 1e300) {
                     double f = 0.0;
