@@ -47,7 +47,7 @@ FP32_MFMA_PEAK = 157.3e12  # FLOP/s, dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 BF16_MFMA_PEAK = 2.5e15    # FLOP/s, dense bf16 MFMA (v_mfma_f32_32x32x16_bf16)
 F64_VALU_PEAK = 78.6e12    # FLOP/s, f64 vector (MI355X spec)
 # per-window PMC figures of the solve kernel (tools/pmc_json.py over tools/gpu_round.sh's passes)
-PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05_solve_pmc.json")
+PMC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_solve_pmc.json")
 
 
 def solve_flop_model(N: int, H: int) -> dict:
