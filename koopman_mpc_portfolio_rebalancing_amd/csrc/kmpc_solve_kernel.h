@@ -422,9 +422,6 @@ __device__ __forceinline__ T gbcast(T v, int src) {
 #ifndef KMPC_OPAQUE_LANE
 #define KMPC_OPAQUE_LANE 1
 #endif
-#ifndef KMPC_LDLT_SPLIT   // the Schur LDL^T with two lanes per row (factor(): one-wave windows' groups of 64)
-#define KMPC_LDLT_SPLIT 0
-#endif
 #ifndef KMPC_RS_BANK   // bank-masked DPP moves for the row_mirror / row_half_mirror levels
 #define KMPC_RS_BANK 1
 #endif
@@ -1605,92 +1602,10 @@ __device__ __forceinline__ bool factor(TH& T, Shared<HM, NWM, typename TH::real_
     // barrier). Unused columns (t >= H, or the cap columns without a cap) become identity rows;
     // I' adds 1 on the a- and v-type diagonals. L is stored strictly lower (zero elsewhere).
     // (the column broadcast of the LDL^T steps uses reduction slots: no reduction is in flight here)
+    // (two lanes per row — even / odd columns, L_rj to the partner by a permlane32 swap — was
+    // bit-identical but measured slower, C3 mixed 79.5 -> 88.0 ms: r06, commit history)
     Real* col = &sh.red[0][0][0];
-    if constexpr (TH::GLN == 64 && KM <= 32 && KMPC_LDLT_SPLIT) {
-        // Two lanes per row (round 6): lane r < 32 holds the even columns of row r, lane 32 + r the
-        // odd ones, so a column step's LDS reads and FMAs are split between the two halves of
-        // wave 0 (about (KM - j) / 2 each instead of KM - 1 - j: 240 instead of 435 per lane over
-        // the factorization at KM = 30). Step j: the half owning column j writes it to LDS, every
-        // lane reads the entries of its own columns, the pivot comes by v_readlane from the owner
-        // of (j, j), L_rj is formed by the owner half and handed to the other by a permlane32
-        // swap. The same operations on every entry, in the same order: the factor is bit-identical
-        // to the one-lane-per-row form's.
-        constexpr int S = (KM + 1) / 2;   // columns per lane
-        if (threadIdx.x < WAVE) {
-            int ln = (int)threadIdx.x;
-#if KMPC_OPAQUE_LANE
-            asm volatile("" : "+v"(ln));
-#endif
-            const int hi = ln >> 5;    // 0: even columns, 1: odd columns
-            const int r = ln & 31;     // the row
-            const bool rused = r < KM && (r % HM) < H && (r / HM != 1 || T.ht);
-            Real g[S];
-#pragma unroll
-            for (int kk = 0; kk < S; ++kk) {
-                const int k = 2 * kk + hi;
-                const bool kused = k < KM && (k % HM) < H && (k / HM != 1 || T.ht);
-                Real v = (r < KM && k <= r && rused && kused) ? sh.G[r * KM + k] : Real(0.0);
-                if (k == r && k < KM) v += (k / HM < 2 || !rused) ? Real(1.0) : Real(0.0);
-                g[kk] = v;
-            }
-            bool bad = false;
-            Real dinv = Real(0.0);
-#pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                const int jo = j & 1, jj = j >> 1;   // the owner half of column j, its slot there
-                const bool own = hi == jo;
-                const Real u = g[jj];                // row r's column j (in the owner half's lanes)
-                // columns k > j of this lane: slots kk >= k0 (k = 2 kk + hi; at kk = k0 with j even
-                // only the odd half's column is past j)
-                Real cv[S];
-                const int k0 = j >> 1;
-                if (j + 1 < KM) {
-                    if (own) col[r] = u;
-                    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                    for (int kk = k0; kk < S; ++kk) {
-                        const int k = 2 * kk + hi;
-                        cv[kk] = (k > j && k < KM) ? col[k] : Real(0.0);
-                    }
-                }
-                const Real d = bcast(u, jo ? 32 + j : j);
-                bad = bad || !(d > Real(0.0)) || !(d < huge_of<Real>());
-                const Real dm = fmax(d, tiny_of<Real>());
-                Real id;
-                if constexpr (sizeof(Real) == 8) {
-                    id = __builtin_amdgcn_rcp(dm);
-                    id = fma(id, fma(-dm, id, Real(1.0)), id);
-                    id = fma(id, fma(-dm, id, Real(1.0)), id);
-                } else {
-                    id = __builtin_amdgcn_rcpf(dm);
-                }
-                const Real lo = (r > j) ? u * id : Real(0.0);   // L_rj (owner half)
-                const Real lp = partner<32>(lo);                // ... from the partner lane
-                const Real l = own ? lo : lp;
-                if (own && r == j) dinv = id;
-                if (own) g[jj] = lo;
-                if (j + 1 < KM) {
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int kk = k0; kk < S; ++kk) {
-                        if (2 * kk + 1 <= j) continue;          // no lane's column is past j
-                        const Real v = fma(-l, cv[kk], g[kk]);
-                        g[kk] = (2 * kk > j) ? v : (hi ? v : g[kk]);   // (k = j: the even half keeps L_rj)
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            if (r < KM) {
-#pragma unroll
-                for (int kk = 0; kk < S; ++kk) {
-                    const int k = 2 * kk + hi;
-                    if (k < KM) sh.G[r * KM + k] = k < r ? g[kk] : Real(0.0);
-                }
-                if ((r & 1) == hi) sh.gid[r] = dinv;
-            }
-            if (bad && ln == 0) sh.flag = 1;
-        }
-    } else if (gvt<TH::GLN>() < WAVE) {
+    if (gvt<TH::GLN>() < WAVE) {
         int r = lane;
 #if KMPC_OPAQUE_LANE
         // a fresh value per call: the lane comparisons of the unrolled steps (r > j, r == j) are
