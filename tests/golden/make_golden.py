@@ -12,7 +12,8 @@ What it records (all float data, no code):
                   long-double oracle optimum
                   (oracle/kmpc_oracle.c), plus SLSQP / dense-IPM cross-checks where small enough.
   headline_*.npz  the bench's models (weights regenerated from their seed by the test) run through
-                  the reference's GenericKM and rebalance op order on 64 windows: obs, stats, yhat.
+                  the reference's GenericKM / LISTAKM and rebalance op order on 64 (c5: 16) windows:
+                  obs, stats, yhat (c5: and the same model in float64).
   backtest_*.npz  reference run_backtest + calculate_metrics (backtest.py:133-249) on a synthetic
                   FinanceEnv built with the reference's data_finance functions; the MPC solve inside
                   KoopmanMPCStrategy is routed to the oracle (cvxpy is not installed here), and every
@@ -232,6 +233,55 @@ def make_headline_goldens():
         print("headline", name, yhat.shape, float(np.abs(yhat).max()))
 
 
+def make_headline_c5():
+    """BASELINE configs[4]'s model (bench.make_lista_state_dict: LISTAKM, linear We, 10 loops,
+    latent 512, obs 10,000, N = 500, H = 20) loaded strictly into the reference's LISTAKM
+    (model.py:804-850, the 'lista' config), 16 windows of bench.secondary_c5's input stream, the
+    reference's rebalance op order in fp32 — and the same model in float64 (the reference modules
+    cast with .double()), the yardstick of both fp32 rollouts at this depth (10 shrink loops, 20
+    latent steps, K = 10,000 dot products: the reference's own fp32 result is ~1e-6 from it)."""
+    import copy
+    import bench
+    N, L, H, emb, xseed = 500, 512, 20, 20, 200
+    obs_n = N * emb
+    sd, lc = bench.make_lista_state_dict(obs_n, L, seed=2)
+    cfg = ref_config.get_config("lista")
+    cfg.MODEL.TARGET_SIZE = L
+    cfg.MODEL.ENCODER.LISTA.L = lc
+    cfg.MODEL.ENCODER.LISTA.NUM_LOOPS = 10
+    cfg.MODEL.ENCODER.LISTA.ALPHA = 5e-3
+    cfg.MODEL.ENCODER.LISTA.LINEAR_ENCODER = True
+    model = ref_model.make_model(cfg, obs_n)
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    mean = np.linspace(-8e-4, 1.2e-3, N)
+    std = np.linspace(0.01, 0.025, N)
+    env = types.SimpleNamespace(n_assets=N, stats=ref_data.FinanceStats(mean, std, [f"A{i}" for i in range(N)]))
+    env.extract_current_returns = types.MethodType(ref_data.FinanceEnv.extract_current_returns, env)
+    env.destandardize_returns = types.MethodType(ref_data.FinanceEnv.destandardize_returns, env)
+    x, _ = bench.window_inputs(0, 16, N, obs_n, seed=xseed, device=torch.device("cpu"))
+    obs = x.numpy().astype(np.float32)
+    yhat = reference_yhat(model, env, obs, H)
+    md = copy.deepcopy(model).double()
+    y64 = []
+    with torch.no_grad():
+        for b in range(obs.shape[0]):
+            z = md.encode(torch.from_numpy(obs[b]).double().unsqueeze(0))
+            ps = []
+            for _ in range(H):
+                z = md.step_latent(z)
+                p = md.decode(z)[..., :N]
+                ps.append((p * torch.from_numpy(std) + torch.from_numpy(mean)).numpy().ravel())
+            y64.append(np.array(ps))
+    y64 = np.stack(y64)
+    meta = {"N": N, "emb": emb, "L": L, "H": H, "weight_seed": 2, "obs_seed": xseed, "lista_L": lc,
+            "checksums": state_checksums(sd), "torch": torch.__version__,
+            "generator": "tests/golden/make_golden.py make_headline_c5"}
+    np.savez_compressed(os.path.join(HERE, "headline_c5.npz"), obs=obs, yhat=yhat, yhat_f64=y64, mean=mean, std=std,
+                        meta=json.dumps(meta))
+    print("headline c5", yhat.shape, float(np.abs(yhat).max()), float(np.abs(yhat - y64).max() / np.abs(yhat).max()))
+
+
 def make_mpc_goldens():
     rng = np.random.default_rng(2024)
     # reference test_mpc cases with their exact optima (tests/test_mpc.py:6-55 of the reference)
@@ -389,6 +439,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["rollout", "mpc", "backtest", "embedding", "dmd", "headline"]
     if "headline" in which:
         make_headline_goldens()
+    if "headline" in which or "headline_c5" in which:
+        make_headline_c5()
     if "dmd" in which:
         make_dmd_goldens()
     if "embedding" in which:
