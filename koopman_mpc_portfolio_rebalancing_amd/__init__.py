@@ -11,4 +11,4 @@ from .koopman import DeviceKoopman, KoopmanModelSpec, standardize_panel  # noqa:
 from .backtest import (BacktestConfig, BuyAndHoldStrategy, KoopmanMPCStrategy, Strategy,  # noqa: F401
                        calculate_metrics, run_backtest, run_backtest_lockstep)
 
-__version__ = "0.4.0"
+__version__ = "0.6.0"
