@@ -23,6 +23,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 MUS = [float(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1e-4,5e-5,2e-5").split(",")]
 REPS = int(os.environ.get("REPS", "3"))
 TOL = float(os.environ.get("TOL", "1e-9"))   # MPCConfig.tol (the interior point's complementarity tolerance)
+NREF = int(os.environ.get("NREF", "0"))      # MPCConfig.n_refine (0: the kernel default, 3; -1: none)
 dev = torch.device("cuda", 0)
 N, L, H = 100, 256, 10
 obs = N * 20
@@ -62,11 +63,11 @@ def vs_oracle(name, W, v):
 
 
 for name, y in (("bench", y_bench), ("random", y_rand)):
-    dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64", tol=TOL))
+    dt, W64, s64, v64, it64 = run(y, MPCConfig(horizon=H, precision="f64", tol=TOL, n_refine=NREF))
     print(f"[{name}] f64: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters {it64.float().mean().item():.2f} "
           f"status {np.bincount(s64.cpu().numpy(), minlength=5)} {vs_oracle(name, W64, v64)}", flush=True)
     for mu in MUS:
-        dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu, tol=TOL))
+        dt, W, s, v, it = run(y, MPCConfig(horizon=H, precision="auto", mu_handoff=mu, tol=TOL, n_refine=NREF))
         ok = (s <= 1) & (s64 <= 1)
         print(f"[{name}] mixed mu_handoff={mu:g}: {dt * 1e3:.2f} ms {B / dt:.0f} win/s iters "
               f"{it.float().mean().item():.2f} status {np.bincount(s.cpu().numpy(), minlength=5)} "
