@@ -77,8 +77,13 @@ extern "C" {
  *          window of a chunk of min(B, 131072) windows: (5 H N + 3 H + 16) floats rounded up to 64 B.
  *          Too little -> KMPC_ERR_WORKSPACE.
  */
-#define KMPC_PATH_AUTO     0   /* kernel chosen by shape (and the closed-form presolve)            */
-#define KMPC_PATH_REGISTER 1   /* interior point in the register kernels where the shape fits them */
+#define KMPC_PATH_AUTO     0   /* kernel chosen by shape and batch (and the closed-form presolve);
+                                  small windows (N <= 32) are packed 2-4 per wave from
+                                  KMPC_PACK_MIN_B windows per call (ABI 0.6.0; any batch for
+                                  H <= 2), one per wave below it — the faster form at each size */
+#define KMPC_PACK_MIN_B    512
+#define KMPC_PATH_REGISTER 1   /* interior point in the register kernels where the shape fits them
+                                  (small windows packed at any batch size)                         */
 #define KMPC_PATH_LARGE    2   /* interior point in the large-window (workspace) kernel            */
 #define KMPC_PATH_REGISTER_UNPACKED 3   /* register kernels, one window per wave even for N <= 32
                                            (no lane-group packing); for A/B and tests             */

@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = ("kmpc_solve", "kmpc_rollout", "kmpc_window", "kmpc_workspace
 PATH_AUTO, PATH_REGISTER, PATH_LARGE, PATH_REGISTER_UNPACKED = 0, 1, 2, 3   # kmpc_solve_desc.path
 PRECISION_AUTO, PRECISION_F64, PRECISION_MIXED = 0, 1, 2   # kmpc_solve_desc.precision
 MIXED_MIN_B = 2048   # KMPC_MIXED_MIN_B: AUTO runs the mixed pair from this many windows per call
+PACK_MIN_B = 512     # KMPC_PACK_MIN_B: AUTO packs N <= 32 windows 2-4 per wave from this many (H > 2)
 
 # ABI of the structs below (include/kmpc.h); 0.2.0 appended kmpc_solve_desc.path and
 # kmpc_rollout_desc.latent_unfused, 0.3.0 kmpc_solve_desc.precision and .mu_handoff, so an older

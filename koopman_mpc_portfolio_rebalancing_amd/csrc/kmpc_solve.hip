@@ -19,9 +19,23 @@ namespace {
 // per-call solver path (kmpc_solve_desc.path): KMPC_PATH_AUTO by shape, KMPC_PATH_REGISTER =
 // interior point in the register kernels whenever they support the shape (no presolve),
 // KMPC_PATH_LARGE = the large-window kernel, KMPC_PATH_REGISTER_UNPACKED = the register kernels
-// with one window per wave even for small windows (no lane-group packing, no presolve)
+// with one window per wave even for small windows (no lane-group packing, no presolve); AUTO and
+// REGISTER pack small windows (pack_small: AUTO from KMPC_PACK_MIN_B windows, REGISTER always)
 bool simplex_case(const SolveArgs& a) {
     return a.path == KMPC_PATH_AUTO && !(a.c > 0.0) && !(a.tau > 0.0) && !a.allow_short;
+}
+
+// Lane-group packing of small windows (N <= 32: 2-4 windows per wave) is a throughput layout. For
+// a batch that cannot fill the GPU a window's latency decides, and one window per wave is faster:
+// AUTO packs only from KMPC_PACK_MIN_B (include/kmpc.h) windows per call (H > 2), or at any batch
+// size for H <= 2.
+// Measured (tools/pack_cross_probe.py, solve only, packed / one-per-wave ms): N = 10, H = 5:
+// B = 256 0.341 / 0.292, 1,024 0.361 / 0.342, 2,048 0.374 / 0.426, 65,536 3.41 / 9.08; N = 20,
+// H = 10: B = 256 0.965 / 0.774, 1,024 1.03 / 1.39; N = 8, H = 2: packed ahead at every B. In the
+// path-persistent backtest (P = 64, N = 10, H = 5): 0.297 -> 0.239 ms per step.
+bool pack_small(const SolveArgs& a) {
+    if (a.path == KMPC_PATH_REGISTER_UNPACKED || a.N > 32 || a.H > 10) return false;
+    return a.path != KMPC_PATH_AUTO || a.B > KMPC_PACK_MIN_B || a.H <= 2;
 }
 
 // c = tau = 0, w >= 0: per period t, log(R_t . w_t) with R = exp(yhat) > 0 is maximized over the
@@ -312,7 +326,7 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
     if (use_big(a)) return big_launch(a, ws, ws_bytes, stream);
 #endif
     // N <= 32: several windows per wave on lane groups (16 lanes for N <= 16 at H <= 5, else 32)
-    if (a.path != KMPC_PATH_REGISTER_UNPACKED && a.N <= 32 && a.H <= 10) {
+    if (pack_small(a)) {
 #ifndef KMPC_DEV_ONLY_H10
         const int rc = a.H <= 2 ? launch_ipm_packed<2>(a, stream)
                                 : (a.H <= 5 ? launch_ipm_packed<5>(a, stream) : launch_ipm_packed<10>(a, stream));
@@ -369,7 +383,7 @@ int backtest_run_launch(const kmpc_backtest_desc* bd, const kmpc_solve_desc* sd,
     d.B = bd->P;
     SolveArgs a = make_args(&d);
     const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
-    const bool packed = a.path != KMPC_PATH_REGISTER_UNPACKED && a.N <= 32 && a.H <= 10;
+    const bool packed = pack_small(a);   // (the kernel kmpc_solve picks for this batch of P windows)
     if (a.return_full || simplex_case(a) || use_big(a) || mixed_case(a, &d) || !fl7 || a.N > 256)
         return KMPC_ERR_UNSUPPORTED;
     // (the packed kernels exist for H = 2, 5, 10 — launch_ipm_packed's HM, exact H only)

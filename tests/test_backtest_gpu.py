@@ -197,28 +197,35 @@ def test_lockstep_path_groups_on_streams_equal_one_group(P, groups):
         assert torch.equal(v, grp["metrics"][k]), k
 
 
-@pytest.mark.parametrize("P,T,chunk,N,H", [(64, 22, None, 100, 10), (61, 19, 128, 100, 10), (24, 14, None, 100, 5),
-                                             (20, 15, None, 50, 10), (16, 14, None, 150, 10), (12, 12, None, 200, 5),
-                                             # packed (N <= 32): one path per lane group
-                                             (64, 30, None, 10, 5), (61, 14, 80, 10, 5), (22, 13, None, 16, 5),
-                                             (21, 13, None, 30, 5), (19, 16, None, 20, 10), (9, 10, None, 8, 2)])
-def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, N, H, monkeypatch):
+@pytest.mark.parametrize("P,T,chunk,N,H,path", [(64, 22, None, 100, 10, 0), (61, 19, 128, 100, 10, 0),
+                                                  (24, 14, None, 100, 5, 0), (20, 15, None, 50, 10, 0),
+                                                  (16, 14, None, 150, 10, 0), (12, 12, None, 200, 5, 0),
+                                                  # packed (N <= 32; KMPC_PATH_REGISTER packs at any batch
+                                                  # size): one path per lane group
+                                                  (64, 30, None, 10, 5, 1), (61, 14, 80, 10, 5, 1),
+                                                  (22, 13, None, 16, 5, 1), (21, 13, None, 30, 5, 1),
+                                                  (19, 16, None, 20, 10, 1), (9, 10, None, 8, 2, 0),
+                                                  # N <= 32 under AUTO below KMPC_PACK_MIN_B paths: one per wave
+                                                  (64, 20, None, 10, 5, 0), (19, 16, None, 20, 10, 0)])
+def test_persistent_backtest_equals_lockstep_loop(P, T, chunk, N, H, path, monkeypatch):
     """run_backtest_lockstep(persistent=True): every step of every path in kmpc_backtest_run launches
     (one workgroup per path: the step's solve, then its bookkeeping, back to back) against the
     lock-step loop (one kmpc_solve over the P windows + one kmpc_backtest_step per step): the same
     window solve and bookkeeping code, so histories, weights and metrics are bit-identical. P = 61
     with 2 steps per rollout chunk: several launches, each resuming the paths' state. The other
     shapes: the constant-case kernels' persistent forms (64-, 128- and 256-thread windows, H = 5),
-    and the packed kernels' (N <= 32: 16-lane groups with 11 or 16 cold slots, 32-lane groups, H = 2 /
+    the packed kernels' (N <= 32: 16-lane groups with 11 or 16 cold slots, 32-lane groups, H = 2 /
     5 / 10; one path per lane group, the bookkeeping's sums as group butterflies — the lock-step
-    kernel's order — with ragged last blocks: P = 61, 22, 21, 19, 9)."""
+    kernel's order — with ragged last blocks: P = 61, 22, 21, 19, 9), and N <= 32 under AUTO below
+    KMPC_PACK_MIN_B paths (one window per wave, as kmpc_solve then runs the step's batch)."""
     import bench
     from koopman_mpc_portfolio_rebalancing_amd import backtest as bt
     dev = torch.device("cuda")
     L = 256
     obs_n = N * 20
     spec = KoopmanModelSpec.from_state_dict(bench.make_state_dict(obs_n, L, 1024, seed=0), bench.MODEL_CFG)
-    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2), device="cuda")
+    strat = KoopmanMPCStrategy(spec, MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, solver_path=path),
+                               device="cuda")
     g = torch.Generator().manual_seed(4)
     x = torch.randn(P, T, obs_n, generator=g).to(dev)
     r = (torch.randn(P, T, N, generator=g) * 0.015 + 5e-4).to(dev)

@@ -212,6 +212,7 @@ def test_python_constants_match_the_header():
     assert defs["KMPC_PRECISION_F64"] == _lib.PRECISION_F64
     assert defs["KMPC_PRECISION_MIXED"] == _lib.PRECISION_MIXED
     assert defs["KMPC_MIXED_MIN_B"] == _lib.MIXED_MIN_B
+    assert defs["KMPC_PACK_MIN_B"] == _lib.PACK_MIN_B
     assert defs["KMPC_DTYPE_F32"] == _lib.DTYPE["fp32"]
     assert defs["KMPC_DTYPE_BF16"] == _lib.DTYPE["bf16"]
     assert defs["KMPC_DTYPE_F32_F32MFMA"] == _lib.DTYPE["fp32_f32mfma"]

@@ -153,7 +153,7 @@ def test_packed_small_windows_match_oracle(N, H, case):
     if tau > 0 and N > 1:
         wp[6] = 0.0
         wp[6, 0] = 3.0                          # sum(w_prev) = 3: the cap makes the budget unreachable
-    path = _lib.PATH_REGISTER if (c == 0.0 and tau == 0.0 and not short) else 0   # (no presolve)
+    path = _lib.PATH_REGISTER   # (packed at any batch size — AUTO packs from KMPC_PACK_MIN_B — and no presolve)
     W, st, val = _solve(wp, y, c, tau, short, path=path)
     W2, st2, val2 = _solve(wp, y, c, tau, short, path=path)
     assert np.array_equal(W, W2) and np.array_equal(st, st2) and np.array_equal(val, val2, equal_nan=True)
