@@ -73,8 +73,9 @@ extern "C" {
  *          kernel keeps each window's interior-point state there: (22 HM + 128) (64 ceil(N / 64))
  *          doubles per window slot, HM = 10 for H <= 10 and 21 past it (the compiled horizon
  *          bound, not H), for min(B, 768) slots when N <= 256, min(B, 512) otherwise.
- *          The mixed-precision pair (AUTO at >= KMPC_MIXED_MIN_B windows, MIXED) keeps one float32 iterate record per
- *          window of a chunk of min(B, 131072) windows: (5 H N + 3 H + 16) floats rounded up to 64 B.
+ *          The mixed-precision pair (AUTO at >= KMPC_MIXED_MIN_B windows, MIXED) keeps a 64 B record
+ *          header per window, B x 64 bytes (ABI 0.6.0: the float32 iterate goes to the float64
+ *          finish on chip; 0.5.0 kept a (5 H N + 3 H + 16)-float record per window).
  *          Too little -> KMPC_ERR_WORKSPACE.
  */
 #define KMPC_PATH_AUTO     0   /* kernel chosen by shape and batch (and the closed-form presolve);

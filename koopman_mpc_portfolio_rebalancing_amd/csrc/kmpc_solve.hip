@@ -259,13 +259,15 @@ SolveArgs make_args(const kmpc_solve_desc* d) {
     a.n_refine = d->n_refine > 0 ? d->n_refine : (d->n_refine < 0 ? 0 : 3);
     a.path = d->path;
     a.warm = nullptr;
+    a.warm_floats = 0;
     a.mu_handoff = d->mu_handoff > 0.0 ? d->mu_handoff : MU_HANDOFF;
     return a;
 }
 
 // Mixed precision (kmpc_solve_kernel.h, PH = 1 / 2): the shapes with a float32 / float64 kernel
 // pair — the C3 kernel's (H = 10, 128 threads with N < 104, no short, c > 0 or tau > 0, cap).
-// Windows go through in chunks of at most WARM_CHUNK, one warm record each.
+// One warm record per window: its 64 B header alone with the fused kernel's on-chip handoff (the
+// whole batch in one launch), else the full record, in chunks of at most WARM_CHUNK windows.
 constexpr int WARM_CHUNK = 131072;
 // AUTO takes the pair from KMPC_MIXED_MIN_B windows: below it a launch is latency-bound (the
 // slowest window's iterations), and float64 alone measured faster — lock-step backtest, C3 model,
@@ -278,10 +280,11 @@ bool mixed_case(const SolveArgs& a, const kmpc_solve_desc* d) {
     const bool fl7 = !a.allow_short && (a.c > 0.0 || a.tau > 0.0) && a.tau > 0.0;
     return fl7 && a.H == 10 && a.N > 64 && a.N < 104;
 }
-size_t warm_bytes(const SolveArgs& a) {
-    const size_t chunk = a.B < WARM_CHUNK ? (size_t)a.B : (size_t)WARM_CHUNK;
-    return sizeof(float) * warm_stride(a.H, a.N) * chunk;
+// windows per mixed launch: the whole batch when the record is the 64 B header alone
+int warm_chunk(const SolveArgs& a) {
+    return mixed_warm_floats(a.H, a.N) == (size_t)WARM_HEAD || a.B < WARM_CHUNK ? a.B : WARM_CHUNK;
 }
+size_t warm_bytes(const SolveArgs& a) { return sizeof(float) * mixed_warm_floats(a.H, a.N) * (size_t)warm_chunk(a); }
 
 bool use_big(const SolveArgs& a) {
 #ifdef KMPC_DEV_ONLY_H10
@@ -338,9 +341,11 @@ int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_pr
         if (!ws || ws_bytes < warm_bytes(a)) return KMPC_ERR_WORKSPACE;
         SolveArgs c = a;
         c.warm = (float*)ws;
+        c.warm_floats = mixed_warm_floats(a.H, a.N);
         const size_t HN = (size_t)a.H * a.N;
-        for (int b0 = 0; b0 < a.B; b0 += WARM_CHUNK) {
-            c.B = a.B - b0 < WARM_CHUNK ? a.B - b0 : WARM_CHUNK;
+        const int chunk = warm_chunk(a);
+        for (int b0 = 0; b0 < a.B; b0 += chunk) {
+            c.B = a.B - b0 < chunk ? a.B - b0 : chunk;
             c.yhat = a.yhat + (size_t)b0 * HN;
             c.wp = a.wp + (size_t)b0 * a.N;
             c.wout = a.wout + (size_t)b0 * (a.return_full ? HN : (size_t)a.N);

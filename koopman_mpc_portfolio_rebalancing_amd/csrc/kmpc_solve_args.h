@@ -19,6 +19,7 @@ struct SolveArgs {
     double* trace;   // debug: per-iteration (mu, rd, pr, step) of problem 0, or null
     // mixed precision (kmpc_solve_kernel.h, PH = 1 / 2): one warm record per window, or null
     float* warm;
+    size_t warm_floats;   // floats per window in warm (mixed_warm_floats)
     double mu_handoff;   // the float32 phase hands its iterate over at mu <= mu_handoff
 };
 
@@ -33,6 +34,9 @@ constexpr int WARM_HEAD = 16;
 __host__ __device__ inline size_t warm_stride(int H, int N) {
     return ((size_t)WARM_HEAD + 5 * (size_t)H * N + 3 * (size_t)H + 15) / 16 * 16;
 }
+// ... of the C3 mixed launcher (kmpc_solve_c3.hip): the header alone when its fused kernel hands
+// the iterate over on chip (the default), the whole record otherwise
+size_t mixed_warm_floats(int H, int N);
 
 constexpr int QL_CS = 104;     // cold-array stride of the 128-thread QL variant (N < QL_CS assets)
 

@@ -67,6 +67,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(1))) 
 #define KMPC_MIXED_FUSED 1
 #endif
 
+size_t mixed_warm_floats(int H, int N) {
+    return KMPC_MIXED_FUSED && KMPC_REG_HANDOFF_ON ? (size_t)WARM_HEAD : warm_stride(H, N);
+}
+
 int launch_ipm_c3(const SolveArgs& a, hipStream_t stream) {
     if (a.warm && KMPC_MIXED_FUSED) {
         const size_t lds = cold_bytes<10, 128, QL_CS, true, 64, 7, double>();

@@ -51,16 +51,20 @@ def test_argument_errors_need_no_gpu():
     d.precision, d.mu_handoff = 0, 1.5       # a handoff past mu = 1 is no handoff
     assert lib.kmpc_solve(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d.mu_handoff = 0.0
-    # the mixed-precision pair (C3 shape) needs one float32 iterate record per window
+    # the mixed-precision pair (C3 shape) needs a 64 B record header per window (the iterate goes
+    # from the float32 phase to the float64 finish on chip), the whole batch at once
     d.B, d.N, d.H, d.cost_coeff, d.max_turnover, d.precision = 1000, 100, 10, 1e-3, 0.2, 2   # MIXED
-    rec = ((16 + 5 * 10 * 100 + 3 * 10 + 15) // 16) * 16 * 4
-    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) >= 1000 * rec
+    rec = 64
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 1000 * rec
+    d.B = 1 << 20
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == (1 << 20) * rec
+    d.B = 1000
     d.precision = 1
     assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 0
     d.precision = 0                          # AUTO: float64 below KMPC_MIXED_MIN_B windows, the pair from it
     assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == 0
     d.B = _lib.MIXED_MIN_B
-    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) >= _lib.MIXED_MIN_B * rec
+    assert lib.kmpc_workspace_bytes(None, ctypes.byref(d)) == _lib.MIXED_MIN_B * rec
     d.B, d.N, d.H, d.cost_coeff, d.max_turnover, d.precision = 0, 5, 5, 0.0, 0.0, 0
     assert lib.kmpc_gross_returns(0, None, None, None) == 0
     assert lib.kmpc_gross_returns(4, None, None, None) == -1

@@ -87,8 +87,8 @@ def test_mixed_handoff_threshold_keeps_parity(mu_handoff):
 
 
 def test_warm_records_chunk_boundary():
-    """Past 131,072 windows the warm records are reused chunk by chunk: windows on either side of
-    the boundary equal the same windows solved alone, bit for bit."""
+    """Past 131,072 windows (the r05 record chunk; one launch with the 64 B header): windows on
+    either side of the boundary equal the same windows solved alone, bit for bit."""
     rng = np.random.default_rng(3)
     B, N, H = 131072 + 96, 100, 10
     wp = rng.dirichlet(np.ones(N), B)
