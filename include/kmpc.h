@@ -100,7 +100,9 @@ extern "C" {
 #define KMPC_PRECISION_MIXED 2
 #define KMPC_MIXED_MIN_B 2048
 typedef struct kmpc_solve_desc {
-    int    B;              /* number of independent problems (windows)           */
+    int    B;              /* number of independent problems (windows); past 2^22
+                              the solve runs as equal launches of <= 2^22 windows
+                              (same kernels, same results as one launch)          */
     int    N;              /* assets,  1 <= N <= KMPC_MAX_N                       */
     int    H;              /* horizon, 1 <= H <= KMPC_MAX_H                       */
     double cost_coeff;     /* MPCConfig.cost_coeff   (mpc.py:22)                  */

@@ -266,6 +266,10 @@ SolveArgs make_args(const kmpc_solve_desc* d) {
 
 // Mixed precision (kmpc_solve_kernel.h, PH = 1 / 2): the shapes with a float32 / float64 kernel
 // pair — the C3 kernel's (H = 10, 128 threads with N < 104, no short, c > 0 or tau > 0, cap).
+// Windows per launch: one workgroup of up to 256 threads per window (the register kernels), so a
+// grid of at most 2^22 stays below a dispatch's 2^32 work-items; larger batches go as equal launches.
+constexpr int LAUNCH_MAX_B = 1 << 22;
+
 // One warm record per window: its 64 B header alone with the fused kernel's on-chip handoff (the
 // whole batch in one launch), else the full record, in chunks of at most WARM_CHUNK windows.
 constexpr int WARM_CHUNK = 131072;
@@ -282,7 +286,8 @@ bool mixed_case(const SolveArgs& a, const kmpc_solve_desc* d) {
 }
 // windows per mixed launch: the whole batch when the record is the 64 B header alone
 int warm_chunk(const SolveArgs& a) {
-    return mixed_warm_floats(a.H, a.N) == (size_t)WARM_HEAD || a.B < WARM_CHUNK ? a.B : WARM_CHUNK;
+    if (mixed_warm_floats(a.H, a.N) == (size_t)WARM_HEAD) return a.B < LAUNCH_MAX_B ? a.B : LAUNCH_MAX_B;
+    return a.B < WARM_CHUNK ? a.B : WARM_CHUNK;
 }
 size_t warm_bytes(const SolveArgs& a) { return sizeof(float) * mixed_warm_floats(a.H, a.N) * (size_t)warm_chunk(a); }
 
@@ -315,6 +320,22 @@ size_t solve_workspace_bytes(const kmpc_solve_desc* d) {
 int solve_launch(const kmpc_solve_desc* d, const float* yhat, const double* w_prev, double* w_out,
                  int* status, double* obj, int* iters, void* ws, size_t ws_bytes, hipStream_t stream,
                  double* trace) {
+    if (d->B > LAUNCH_MAX_B) {
+        // equal launches of at most LAUNCH_MAX_B windows: each chunk is past every batch threshold
+        // (KMPC_MIXED_MIN_B, KMPC_PACK_MIN_B), so AUTO takes the same kernels as for the whole batch
+        const int nch = (int)(((size_t)d->B + LAUNCH_MAX_B - 1) / LAUNCH_MAX_B);
+        const int per = (int)(((size_t)d->B + nch - 1) / nch);
+        const size_t HN = (size_t)d->H * d->N, wo = d->return_full_W ? HN : (size_t)d->N;
+        kmpc_solve_desc c = *d;
+        for (int b0 = 0; b0 < d->B; b0 += per) {
+            c.B = d->B - b0 < per ? d->B - b0 : per;
+            const int rc = solve_launch(&c, yhat + (size_t)b0 * HN, w_prev + (size_t)b0 * d->N, w_out + (size_t)b0 * wo,
+                                        status + b0, obj + b0, iters ? iters + b0 : nullptr, ws, ws_bytes, stream,
+                                        b0 == 0 ? trace : nullptr);
+            if (rc != KMPC_OK) return rc;
+        }
+        return KMPC_OK;
+    }
     SolveArgs a = make_args(d);
     a.yhat = yhat; a.wp = w_prev; a.wout = w_out; a.status = status; a.obj = obj; a.iters = iters;
     a.trace = trace;

@@ -6,7 +6,7 @@ within 1e-6 + 1e-5 |f*| of the long-double oracle, W[0] within 1e-3 (c > 0: uniq
 feasibility to 1e-8 — the float32 phase only chooses the starting point of the float64 iteration.
 
 Also BASELINE configs[3]'s per-rank workload (131,072 windows per rank at N = 8) on one
-GPU, and a batch past the 131,072-window chunk of the warm records.
+GPU, a batch past 131,072 windows (the r05 warm-record chunk) and one past 2^22 (two launches).
 """
 import numpy as np
 import pytest
@@ -99,6 +99,27 @@ def test_warm_records_chunk_boundary():
     lo = 131072 - 32
     W1, st1, val1, it1 = _solve(wp[lo:], y[lo:], cfg)
     assert np.array_equal(W1, W[lo:]) and np.array_equal(val1, val[lo:]) and np.array_equal(it1, it[lo:])
+
+
+def test_launch_split_past_4m_windows():
+    """Past 2^22 windows a solve goes as equal launches (a dispatch's grid stays below 2^32
+    work-items): 2^22 + 64 windows at the C3 shape (mixed precision, generated on the device) —
+    every window optimal, and the windows either side of the split equal the same windows solved
+    alone, bit for bit."""
+    B, N, H = (1 << 22) + 64, 100, 10
+    g = torch.Generator(device="cuda").manual_seed(5)
+    y = (torch.randn(B, H, N, generator=g, device="cuda") * 0.015 + 5e-4).float()
+    wp = -torch.rand(B, N, generator=g, device="cuda", dtype=torch.float64).log()
+    wp /= wp.sum(1, keepdim=True)
+    cfg = MPCConfig(horizon=H, cost_coeff=1e-3, max_turnover=0.2, precision="mixed")
+    W, st, val, it = solve_mpc_log_utility_batched(wp, y, cfg, with_iters=True)
+    assert int((st != 0).sum()) == 0
+    split = (B + 1) // 2
+    lo, hi = split - 2048, split + 2048
+    W1, st1, val1, it1 = solve_mpc_log_utility_batched(wp[lo:hi].contiguous(), y[lo:hi].contiguous(), cfg,
+                                                       with_iters=True)
+    assert torch.equal(W1, W[lo:hi]) and torch.equal(val1, val[lo:hi]) and torch.equal(it1, it[lo:hi])
+    del y, wp, W
 
 
 def test_config3_per_rank_workload_on_one_gpu():
