@@ -1553,9 +1553,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                         s = hs ? fabs(d) + 1.0 / N : 0.0;
                         W.at(A_W, t) = w0;
                         W.at(A_S, t) = s;
-                        W.at(A_L1, t) = hw ? 1.0 : 0.0;
-                        W.at(A_L2, t) = hs ? 1.0 : 0.0;
-                        W.at(A_L3, t) = hs ? 1.0 : 0.0;
+                        W.at(A_L1, t) = hw ? KMPC_INIT_MULT : 0.0;
+                        W.at(A_L2, t) = hs ? KMPC_INIT_MULT : 0.0;
+                        W.at(A_L3, t) = hs ? KMPC_INIT_MULT : 0.0;
                     }
                     W.slot(t, s);
                 }
@@ -1563,7 +1563,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
                 if (threadIdx.x < HM) {
                     const int t = threadIdx.x;
                     sh.z4[t] = (ht && t < H) ? fmax(a.tau - sh.tot[t], 0.5 * a.tau) : 1.0;
-                    sh.l4[t] = (ht && t < H) ? 1.0 : 0.0;
+                    sh.l4[t] = (ht && t < H) ? KMPC_INIT_MULT : 0.0;
                     sh.nu[t] = 0.0;
                 }
                 __syncthreads();

@@ -117,6 +117,13 @@ constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
 // is ill-conditioned one iteration earlier (an unrefined corrector at mu ~ 1.5e-6 left dual
 // residuals of 3e-6 and an optimal_inaccurate status in float64). Without shorting 1e-5 only adds
 // refinement passes (C3 solve -3%, measured r03).
+#ifndef KMPC_INIT_MULT   // the initial point's multipliers (l1, l2, l3, l4; the oracle's too)
+#define KMPC_INIT_MULT 0.5
+#endif
+// 0.5 since round 6 (was 1): the dual start sits nearer the scaled problem's multipliers, ~0.4 fewer
+// iterations at C3 (15.65 -> 15.24 on the bench's windows: C3 798.6 k -> 817.8 k windows/s), 0.63
+// at C5 (25.62 -> 24.99: 61.4 -> 60.6 ms), 0.35 on configs[0]'s shape; same statuses
+// (tools/gpu_r6s.sh; measured on the oracle first: 0.4 and 0.5 best of 0.1-3)
 #ifndef KMPC_REFINE_MU
 #define KMPC_REFINE_MU 1e-6
 #endif
