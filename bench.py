@@ -155,7 +155,7 @@ MODEL_CFG = {"MODEL": {"MODEL_NAME": "GenericKM", "NORM_FN": "id",
 def make_inputs(B: int, N: int, obs: int, seed: int, device):
     g = torch.Generator(device="cpu").manual_seed(seed)
     x = torch.randn(B, obs, generator=g)                                   # standardized embedding
-    wp = torch.distributions.Dirichlet(torch.ones(N, dtype=torch.float64)).sample((B,))  # uses global RNG
+    wp = torch.from_numpy(np.random.default_rng(seed).dirichlet(np.ones(N), B))   # seeded too
     return x.to(device), wp.to(device)
 
 

@@ -1,5 +1,5 @@
 """Dev probe (GPU): the large-window launch's tail at C5 (N = 500, H = 20; BASELINE configs[4]).
-The secondary_c5 workload (bench's LISTAKM model, fp32 rollout, 1,024 windows) solved once with
+The secondary_c5 workload (bench's LISTAKM model, fp32 rollout, 1,024 windows; DT=bf16: the bench's bf16 rollout) solved once with
 iteration counts: their distribution, the static slot schedule's makespan (slot s runs windows
 s, s + slots, ... in iterations) against the mean, and the launch time at B = 256 / 512 / 768 /
 1,024 / 2,048 windows (random yhat for the sizes past the workload's batch)."""
@@ -17,7 +17,7 @@ obs = N * 20
 sd, lc = bench.make_lista_state_dict(obs, L, seed=2)
 cfg_m = {"MODEL": {"MODEL_NAME": "LISTAKM", "NORM_FN": "id",
                    "ENCODER": {"LISTA": {"ALPHA": 5e-3, "L": lc, "NUM_LOOPS": 10}}}}
-model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, cfg_m), dev, dtype="fp32")
+model = DeviceKoopman(KoopmanModelSpec.from_state_dict(sd, cfg_m), dev, dtype=os.environ.get("DT", "fp32"))
 mean_d = torch.full((N,), 5e-4, dtype=torch.float32, device=dev)
 std_d = torch.full((N,), 0.015, dtype=torch.float32, device=dev)
 x, wp = bench.make_inputs(B, N, obs, seed=200, device=dev)
