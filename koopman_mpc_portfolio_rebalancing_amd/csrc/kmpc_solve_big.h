@@ -1425,13 +1425,14 @@ __device__ __forceinline__ int ipm_iterate(Win<HM, FL>& W, double* wout, int tw,
             ph_newton(W, (pass == 0 || mu > (W.hw() ? REFINE_MU : REFINE_MU_SHORT)) ? 0 : a.n_refine, pass == 1, smu);
             double cc1, cc2;
             const double amax = ph_step(W, cc1, cc2, pass == 0, smu);
-            if (pass == 1) { step = fmin(1.0, 0.99 * amax); break; }
+            if (pass == 1) { step = fmin(1.0, (W.hw() ? KMPC_STEP_NOSHORT : 0.99) * amax); break; }
             const double ap = fmin(1.0, amax);
             double comp = mu_l + ap * (cc1 + ap * cc2);
             if (W.ht())
                 for (int t = 0; t < H; ++t) comp += (sh.z4[t] + ap * sh.dz4[t]) * (sh.l4[t] + ap * sh.dl4[t]);
             double sg = comp * inv_ncon / mu;
             sg = sg * sg * sg;
+            if (W.hw() && W.ht()) sg = fmin(sg, KMPC_SIGMA_CAP);
             smu = sg * mu;   // the corrector's targets are formed inside its first solve
         }
         if (a.trace && b == 0 && threadIdx.x == 0) a.trace[4 * it + 3] = step;

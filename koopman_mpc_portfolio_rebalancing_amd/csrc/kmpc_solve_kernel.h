@@ -124,6 +124,17 @@ constexpr double REFINE_RTOL = KMPC_REFINE_RTOL;
 // iterations at C3 (15.65 -> 15.24 on the bench's windows: C3 798.6 k -> 817.8 k windows/s), 0.63
 // at C5 (25.62 -> 24.99: 61.4 -> 60.6 ms), 0.35 on configs[0]'s shape; same statuses
 // (tools/gpu_r6s.sh; measured on the oracle first: 0.4 and 0.5 best of 0.1-3)
+// Step and centring rules for the no-short problems (the oracle's too): the step goes to 0.995 of
+// the boundary (0.99 with shorting, where the free w makes the end-game ill-conditioned: 0.995 left
+// more windows optimal_inaccurate there), and with the turnover cap the centring parameter
+// sigma = (mu_aff / mu)^3 is capped at 0.2 (without the cap the capped sigma cost iterations).
+// Round 6, measured on the oracle over 15 shapes, then on the device: DESIGN §3.2.
+#ifndef KMPC_STEP_NOSHORT
+#define KMPC_STEP_NOSHORT 0.995
+#endif
+#ifndef KMPC_SIGMA_CAP
+#define KMPC_SIGMA_CAP 0.2
+#endif
 #ifndef KMPC_REFINE_MU
 #define KMPC_REFINE_MU 1e-6
 #endif

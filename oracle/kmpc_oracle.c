@@ -73,6 +73,8 @@ typedef double real;
 #endif
 #define RISFIN(x) isfinite(x)
 #define KMPC_INIT_MULT R_(0.5)   /* the initial point's multipliers, as the kernels' KMPC_INIT_MULT */
+#define KMPC_SIGMA_CAP R_(0.2)   /* as the kernels' (kmpc_solve_kernel.h) */
+#define KMPC_STEP_NOSHORT R_(0.995)
 
 /*
  * numpy's float32 exp (numpy 2.x, x86-64 AVX2 / AVX512F: simd_exp_f32 in
@@ -664,6 +666,8 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
             real ap = RFMIN(1, max_step(&W));
             real sg = complementarity(&W, ap) / ncon / mu;
             sg = sg * sg * sg;
+            /* no short + turnover cap: sigma capped at 0.2 (the kernels' KMPC_SIGMA_CAP, round 6) */
+            if (W.hw && W.ht && sg > KMPC_SIGMA_CAP) sg = KMPC_SIGMA_CAP;
             /* corrector: rc = z l + dz_aff dl_aff - sigma mu */
             for (int t = 0; t < H; ++t) {
                 for (int i = 0; i < N; ++i) {
@@ -685,8 +689,9 @@ int API(kmpc_oracle_solve)(int N, int H, const double* wp, const float* yhat, do
                 W.n_refine = nr;
             }
             /* one step length for primal and dual: the objective is nonlinear, so unequal steps
-               would re-inject dual residual (alpha_p - alpha_d) Hf dw */
-            real a = RFMIN(1, R_(0.99) * max_step(&W));
+               would re-inject dual residual (alpha_p - alpha_d) Hf dw. 0.995 of the boundary
+               without shorting, 0.99 with it (the kernels' KMPC_STEP_NOSHORT, round 6) */
+            real a = RFMIN(1, (W.hw ? KMPC_STEP_NOSHORT : R_(0.99)) * max_step(&W));
             for (size_t k = 0; k < HN; ++k) {
                 W.w[k] += a * W.dw[k]; W.s[k] += a * W.ds[k];
                 W.l1[k] += a * W.dl1[k]; W.l2[k] += a * W.dl2[k]; W.l3[k] += a * W.dl3[k];
