@@ -780,7 +780,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "strong" if c4 else "weak", "vs_baseline": None,
             "dtype": "f32 rollout (fp32 GEMMs as three exact bf16 planes); mixed f32->f64 IPM solve "
-                     "(float32 phase to mu 5e-5, float64 finish: stopping rule, status and W in float64)",
+                     "(float32 phase to mu 3e-5, float64 finish: stopping rule, status and W in float64)",
             "data": "synthetic (seeded N(0,1) standardized embeddings, Dirichlet w_prev, random-init finance_sparse weights)",
             "config": {"workload": (f"C4 (BASELINE configs[3]): {G} windows/step over {world} GPUs" if c4 else
                                     f"C3 (BASELINE configs[2]): {G} windows/GPU") +

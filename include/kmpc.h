@@ -117,7 +117,7 @@ typedef struct kmpc_solve_desc {
     int    precision;      /* KMPC_PRECISION_* (ABI 0.3.0; MIXED 0.4.0)                           */
     double mu_handoff;     /* mixed precision: the float32 phase hands its iterate to the float64
                               solve once the scaled complementarity mu <= mu_handoff
-                              (<= 0 -> default 5e-5)                                               */
+                              (<= 0 -> default 3e-5)                                               */
 } kmpc_solve_desc;
 
 int kmpc_solve(const kmpc_solve_desc* desc,

@@ -63,8 +63,11 @@ constexpr int SIMPLEX_HR = 16;     // register fast path: N <= 64 assets, H <= 1
 // (tools/f32phase_probe.py, 512 C3 windows of the bench's distribution: float32 to mu <= 5e-5 takes
 // 7.9 of the 15.9 iterations, every window optimal, float64 finish 8.0 iterations; 2e-5 left 1% of
 // the windows optimal_inaccurate) and on MI355X (tools/ab_mixed.sh, 65,536 windows, retry pass in:
-// bench yhat 83.3 ms at 1e-4, 82.0 ms at 5e-5; random yhat 91.1 / 90.7 ms, same statuses as float64)
-constexpr double MU_HANDOFF = 5e-5;
+// bench yhat 83.3 ms at 1e-4, 82.0 ms at 5e-5; random yhat 91.1 / 90.7 ms, same statuses as float64).
+// 3e-5 since round 6's step / sigma rules (tools/gpu_r6v.sh, twice: bench yhat 74.80 / 74.70 ms at
+// 5e-5, 74.43 / 74.24 at 3e-5, 74.11 / 73.94 at 2e-5; random yhat 77.92 / 77.75, 77.64 / 77.45,
+// 78.88 / 78.69 — 2e-5 loses on random yhat; statuses as float64 at every threshold)
+constexpr double MU_HANDOFF = 3e-5;
 
 // butterflies within aligned groups of G lanes (G = 32 or 64)
 template <int G>

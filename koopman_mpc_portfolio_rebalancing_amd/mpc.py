@@ -36,7 +36,7 @@ class MPCConfig:
     n_refine: int = 0  # 0 -> kernel default
     solver_path: int = 0  # kmpc_solve_desc.path: 0 by shape, 1 register IPM (no presolve), 2 large-window IPM, 3 register IPM without lane-group packing
     precision: str = "auto"  # kmpc_solve_desc.precision: "mixed" (float32 warm-start phase + float64 finish where available), "f64", or "auto" (mixed from 2,048 windows per call, else f64)
-    mu_handoff: float = 0.0  # float32 -> float64 handoff at mu <= mu_handoff (0 -> kernel default 5e-5)
+    mu_handoff: float = 0.0  # float32 -> float64 handoff at mu <= mu_handoff (0 -> kernel default 3e-5)
 
 
 def _solve_desc(B: int, N: int, H: int, config: MPCConfig, full: bool) -> _lib.SolveDesc:
