@@ -223,3 +223,16 @@ def test_python_constants_match_the_header():
     assert defs["KMPC_LATENT_AUTO"] == _lib.LATENT_FORM["auto"]
     assert defs["KMPC_LATENT_UNFUSED"] == _lib.LATENT_FORM["unfused"]
     assert defs["KMPC_LATENT_SEQUENTIAL"] == _lib.LATENT_FORM["sequential"]
+
+
+def test_oracle_and_kernels_share_the_iteration_constants():
+    """The kernels run the oracle's iteration: the initial multipliers, the no-short
+    step factor and the capped-sigma bound are the same numbers in kmpc_solve_kernel.h and
+    oracle/kmpc_oracle.c (the device's iteration counts track the oracle's, test_solver_gpu.py)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "koopman_mpc_portfolio_rebalancing_amd", "csrc", "kmpc_solve_kernel.h")).read()
+    orc = open(os.path.join(root, "oracle", "kmpc_oracle.c")).read()
+    for name in ("KMPC_INIT_MULT", "KMPC_SIGMA_CAP", "KMPC_STEP_NOSHORT"):
+        k = float(re.search(r"#define %s ([0-9.e-]+)" % name, hdr).group(1))
+        o = float(re.search(r"#define %s R_\(([0-9.e-]+)\)" % name, orc).group(1))
+        assert k == o, (name, k, o)
